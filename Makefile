@@ -1,0 +1,49 @@
+# jpge build (no cmake needed).  `make -j8` builds:
+#   jpgenc_amd/lib/libjpge.so   the product: HIP kernels for gfx950 + host C++ + C ABI
+#   jpgenc_amd/bin/jpgenc       the CLI (reference main.cpp contract)
+#   oracle/build/liborc.so      test-only CPU restatement (+ oracle/_ref when /root/reference exists)
+ROCM     ?= /opt/rocm
+HIPCC    ?= $(ROCM)/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+BUILD    := build/obj
+SRC      := jpgenc_amd/csrc
+LIBDIR   := jpgenc_amd/lib
+BINDIR   := jpgenc_amd/bin
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SRC) -Iinclude
+CXXFLAGS := -O2 -std=c++17 -fPIC -fopenmp -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
+            -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude
+
+HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp
+HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))
+DEV_OBJS  := $(BUILD)/kernels.o
+HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h
+
+all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc oracle
+
+$(BUILD)/kernels.o: $(SRC)/kernels.hip $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: $(SRC)/%.cpp $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIBDIR)/libjpge.so: $(DEV_OBJS) $(HOST_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fopenmp -o $@ $^ -L$(ROCM)/lib -lamdhip64
+
+$(BINDIR)/jpgenc: $(SRC)/cli.cpp $(LIBDIR)/libjpge.so
+	@mkdir -p $(BINDIR)
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -ljpge -Wl,-rpath,'$$ORIGIN/../lib' \
+	  -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIBDIR) $(BINDIR)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,140 @@
+/*
+ * jpge — MI355X-native JPEG baseline encoder, C ABI (the drop-in boundary).
+ *
+ * The reference (Nuos/jpgEnc) has no FFI: its encode path is the C++ API of the
+ * static library jpgEncLib (src/CMakeLists.txt:6-11) consumed by src/main.cpp.
+ * Each entry point below replaces one piece of that API; the C++ facade in
+ * jpgenc_amd/csrc/jpge_image.hpp re-exposes them under the reference's names.
+ *
+ * Conventions: every function returns a jpge_status (0 = ok); no exceptions or
+ * C++ types cross this boundary; all buffers are owned by the caller; a context
+ * (one HIP device + its streams and workspace) must not be used from two
+ * threads at once.  Output bytes are bit-identical to the reference encoder.
+ */
+#ifndef JPGE_H_
+#define JPGE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    JPGE_OK = 0,
+    JPGE_E_ARG = 1,       /* invalid argument */
+    JPGE_E_NOSPACE = 2,   /* output buffer too small; *len receives the size needed */
+    JPGE_E_HIP = 3,       /* HIP runtime failure */
+    JPGE_E_NODEV = 4,     /* no GPU / bad device index */
+    JPGE_E_FORMAT = 5,    /* not a P3/P6 PPM (reference: std::runtime_error, Image.cpp:449-450) */
+    JPGE_E_IO = 6,        /* cannot open/read/write a file (Image.cpp:427-428) */
+    JPGE_E_TRUNC = 7,     /* PPM sample data shorter than width*height*3 */
+    JPGE_E_RANGE = 8,     /* maxval outside 1..255 (Image.cpp:462) or sample > 255 */
+    JPGE_E_TIMEOUT = 9,   /* device-side scan protocol did not complete */
+    JPGE_E_RCCL = 10,     /* RCCL failure (multi-GPU paths) */
+    JPGE_E_INTERNAL = 11
+} jpge_status;
+
+#define JPGE_DEVICE_INPUT 1u  /* rgb points to device memory */
+#define JPGE_DEVICE_OUTPUT 2u /* out points to device memory */
+
+typedef struct jpge_ctx jpge_ctx;
+
+/* One frame of a batch (jpge_encode_batch). */
+typedef struct {
+    const uint8_t* rgb; /* interleaved RGB8 (host, or device with JPGE_DEVICE_INPUT) */
+    uint32_t width, height;
+    size_t stride;      /* bytes per row, 0 = width*3 */
+    int maxval;         /* PPM maxval, 1..255; samples are scaled by 255./maxval (Image.cpp:465) */
+    uint8_t* out;       /* .jpg destination */
+    size_t cap;         /* capacity of out */
+    size_t len;         /* [out] bytes written */
+    int status;         /* [out] jpge_status of this frame */
+} jpge_frame;
+
+/* Per-kernel device times of the last frame (ms, HIP events on the encode stream). */
+typedef struct {
+    float fdct;     /* K1: colour + 4:2:0 + FDCT + quantise + AC statistics */
+    float dc_stats; /* K2: DC difference statistics */
+    float entropy;  /* K3: RLE/category/Huffman emission + MCU interleave + stuffing */
+    float total;    /* first kernel start .. entropy end (includes the host table build) */
+    double fdct_sum, dc_stats_sum, entropy_sum; /* accumulated since jpge_reset_timing (ms) */
+    uint64_t frames;                            /* frames accumulated */
+} jpge_timing;
+
+const char* jpge_strerror(int status);
+int jpge_version(void);
+int jpge_device_count(int* n);
+
+/* Context lifetime (replaces nothing in the reference: its encoder is stateless). */
+int jpge_open(int device, jpge_ctx** ctx);
+int jpge_close(jpge_ctx* ctx);
+int jpge_set_timing(jpge_ctx* ctx, int on);
+int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t);
+int jpge_reset_timing(jpge_ctx* ctx);
+
+/* Worst-case .jpg size for a frame (header + 2x worst-case entropy + EOI). */
+size_t jpge_max_jpeg_bytes(uint32_t width, uint32_t height);
+
+/* Quantisation tables for quality 1..100: the reference's Annex-K tables
+ * (Image.cpp:850-869) scaled by the IJG rule; quality 50 returns them unchanged,
+ * which is the only table pair the reference itself uses. Natural order. */
+int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]);
+
+/* Full encode — replaces Image::writeJPEG (Image.hpp:92, Image.cpp:831-976) for an
+ * image as produced by loadPPM: SOI APP0 DQT DQT SOF0 DHTx4 SOS <entropy> EOI. */
+int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
+                     int maxval, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
+                     size_t* len, uint32_t flags);
+
+/* Many independent frames, pipelined over the context's streams (configs 3/4). */
+int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
+                      uint32_t flags);
+
+/* Stage entry — convertToColorSpace + applySubsampling(S420_m) + applyDCT(Arai) +
+ * applyQuantization (Image.cpp:839-871) on the GPU: quantised coefficients before
+ * DC differencing, per component, blocks in raster order, 64 natural-order values
+ * per block (host buffers of (W'/8)(H'/8)*64 and 2 x (W'/16)(H'/16)*64 int16). */
+int jpge_fdct_quant(jpge_ctx* ctx, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
+                    int maxval, const uint8_t qy[64], const uint8_t qc[64], int16_t* coef_y, int16_t* coef_cb,
+                    int16_t* coef_cr, uint32_t flags);
+
+/* Stage entry — the symbol "texts" of writeJPEG (Image.cpp:888-906) as histograms:
+ * counts[t*256+s] and first[t*256+s] = position key of the first occurrence
+ * (~0 if absent); t = 0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC. */
+int jpge_symbol_stats(jpge_ctx* ctx, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
+                      int maxval, const uint8_t qy[64], const uint8_t qc[64], uint32_t counts[1024],
+                      uint64_t first[1024], uint32_t flags);
+
+/* Host table build — replaces generateHuffmanCode (Huffman.hpp:53, Huffman.cpp:3-66)
+ * for byte symbols given counts and first-occurrence keys.  bits[0..15] = number
+ * of codes of length 1..16, huffval = DHT symbol order, code/len per symbol. */
+int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], uint8_t bits[16],
+                       uint8_t huffval[256], int* nsym, uint32_t code[256], uint8_t len[256]);
+
+/* Same for an arbitrary int symbol text (the reference signature, for tests and
+ * tools): writes n distinct symbols as (symbol, length, code) in DHT order. */
+int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t* codes, int* nsym);
+
+/* PPM front end — replaces loadPPM (Image.hpp:28, Image.cpp:421-538) up to the
+ * padding, which the GPU path performs by clamped addressing.  parse: rgb gets
+ * width*height*3 unscaled samples (cap bytes available). */
+int jpge_parse_ppm(const uint8_t* buf, size_t n, uint8_t* rgb, size_t cap, uint32_t* width, uint32_t* height,
+                   int* maxval);
+int jpge_ppm_info(const uint8_t* buf, size_t n, uint32_t* width, uint32_t* height, int* maxval);
+
+/* Convenience: PPM file -> .jpg file at the given quality (the CLI path, main.cpp:8-32). */
+int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, int quality);
+
+/* Deterministic synthetic frame (kind 0 photo-like, 1 random bytes, 2 flat). */
+int jpge_synth_rgb8(uint64_t seed, uint32_t width, uint32_t height, int kind, uint8_t* out, size_t stride);
+
+/* The Arai constants compiled into the kernels (Dct.hpp:21-43), for verification:
+ * a[0..4] = a1..a5, s[0..7] = s0..s7. */
+void jpge_arai_constants(double a[5], double s[8]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JPGE_H_ */

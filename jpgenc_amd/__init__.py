@@ -1,0 +1,315 @@
+"""jpge — MI355X-native JPEG baseline encoder (Python side of the C ABI).
+
+This module is a thin ctypes binding over ``jpgenc_amd/lib/libjpge.so`` (the
+HIP kernels + host C++; see ``include/jpge.h``).  It mirrors the reference's
+entry points — ``load_ppm`` (Image.hpp:28 ``loadPPM``) and
+``Encoder.encode`` / ``write_jpeg`` (Image.hpp:92 ``Image::writeJPEG``) — and
+raises ``JpgeError`` (a ``RuntimeError``, the reference's ``std::runtime_error``
+convention, Image.cpp:428/450) on failure.  There is no CPU fallback: if the
+library or a GPU is missing, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libjpge.so")
+
+JPGE_DEVICE_INPUT = 1
+JPGE_DEVICE_OUTPUT = 2
+
+STATUS = {
+    0: "JPGE_OK", 1: "JPGE_E_ARG", 2: "JPGE_E_NOSPACE", 3: "JPGE_E_HIP", 4: "JPGE_E_NODEV",
+    5: "JPGE_E_FORMAT", 6: "JPGE_E_IO", 7: "JPGE_E_TRUNC", 8: "JPGE_E_RANGE", 9: "JPGE_E_TIMEOUT",
+    10: "JPGE_E_RCCL", 11: "JPGE_E_INTERNAL",
+}
+
+# every symbol include/jpge.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_close", "jpge_set_timing",
+    "jpge_get_timing", "jpge_reset_timing", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
+    "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
+    "jpge_ppm_info", "jpge_encode_file", "jpge_synth_rgb8", "jpge_arai_constants",
+)
+
+
+class JpgeError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = lib().jpge_strerror(status).decode() if _LIB is not None else STATUS.get(status, str(status))
+        super().__init__(f"{what}: {STATUS.get(status, status)} ({msg})" if what else msg)
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [
+        ("rgb", ctypes.c_void_p), ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+        ("stride", ctypes.c_size_t), ("maxval", ctypes.c_int), ("out", ctypes.c_void_p),
+        ("cap", ctypes.c_size_t), ("len", ctypes.c_size_t), ("status", ctypes.c_int),
+    ]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("fdct", ctypes.c_float), ("dc_stats", ctypes.c_float), ("entropy", ctypes.c_float),
+                ("total", ctypes.c_float), ("fdct_sum", ctypes.c_double), ("dc_stats_sum", ctypes.c_double),
+                ("entropy_sum", ctypes.c_double), ("frames", ctypes.c_uint64)]
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libjpge.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, sz, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_int
+        L.jpge_strerror.restype = ctypes.c_char_p
+        L.jpge_strerror.argtypes = [i32]
+        L.jpge_open.argtypes = [i32, ctypes.POINTER(vp)]
+        L.jpge_close.argtypes = [vp]
+        L.jpge_set_timing.argtypes = [vp, i32]
+        L.jpge_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
+        L.jpge_reset_timing.argtypes = [vp]
+        L.jpge_device_count.argtypes = [ctypes.POINTER(i32)]
+        L.jpge_max_jpeg_bytes.restype = sz
+        L.jpge_max_jpeg_bytes.argtypes = [u32, u32]
+        L.jpge_quality_tables.argtypes = [i32, vp, vp]
+        L.jpge_encode_rgb8.argtypes = [vp, vp, u32, u32, sz, i32, vp, vp, vp, sz, ctypes.POINTER(sz), u32]
+        L.jpge_encode_batch.argtypes = [vp, ctypes.POINTER(Frame), i32, vp, vp, u32]
+        L.jpge_fdct_quant.argtypes = [vp, vp, u32, u32, sz, i32, vp, vp, vp, vp, vp, u32]
+        L.jpge_symbol_stats.argtypes = [vp, vp, u32, u32, sz, i32, vp, vp, vp, vp, u32]
+        L.jpge_huffman_table.argtypes = [vp, vp, vp, vp, ctypes.POINTER(i32), vp, vp]
+        L.jpge_huffman_text.argtypes = [vp, sz, vp, vp, vp, ctypes.POINTER(i32)]
+        L.jpge_parse_ppm.argtypes = [vp, sz, vp, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                     ctypes.POINTER(i32)]
+        L.jpge_ppm_info.argtypes = [vp, sz, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(i32)]
+        L.jpge_encode_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, i32]
+        L.jpge_synth_rgb8.argtypes = [ctypes.c_uint64, u32, u32, i32, vp, sz]
+        L.jpge_arai_constants.argtypes = [vp, vp]
+        L.jpge_arai_constants.restype = None
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _check(st: int, what: str) -> None:
+    if st != 0:
+        raise JpgeError(st, what)
+
+
+def quality_tables(quality: int = 50) -> tuple[np.ndarray, np.ndarray]:
+    """Annex-K tables scaled for `quality` (50 = the reference's tables, Image.cpp:850-869)."""
+    qy = np.zeros(64, np.uint8)
+    qc = np.zeros(64, np.uint8)
+    _check(lib().jpge_quality_tables(int(quality), _p(qy), _p(qc)), "quality_tables")
+    return qy, qc
+
+
+def synth_rgb8(seed: int, width: int, height: int, kind: int = 0) -> np.ndarray:
+    """Deterministic synthetic frame (H, W, 3) uint8: 0 photo-like, 1 random bytes, 2 flat."""
+    out = np.empty((height, width, 3), np.uint8)
+    _check(lib().jpge_synth_rgb8(seed, width, height, kind, _p(out), width * 3), "synth_rgb8")
+    return out
+
+
+@dataclass
+class PPM:
+    rgb: np.ndarray  # (H, W, 3) uint8, unscaled samples
+    maxval: int
+
+    @property
+    def width(self) -> int:
+        return self.rgb.shape[1]
+
+    @property
+    def height(self) -> int:
+        return self.rgb.shape[0]
+
+
+def parse_ppm(data: bytes) -> PPM:
+    """P3/P6 parser with the reference's tokenizer semantics (Image.cpp:334-474)."""
+    buf = np.frombuffer(data, np.uint8)
+    w, h, mv = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+    _check(lib().jpge_ppm_info(_p(buf), buf.size, ctypes.byref(w), ctypes.byref(h), ctypes.byref(mv)),
+           "parse_ppm")
+    rgb = np.empty((h.value, w.value, 3), np.uint8)
+    _check(lib().jpge_parse_ppm(_p(buf), buf.size, _p(rgb), rgb.size, ctypes.byref(w), ctypes.byref(h),
+                                ctypes.byref(mv)), "parse_ppm")
+    return PPM(rgb, mv.value)
+
+
+def load_ppm(path: str) -> PPM:
+    """loadPPM (Image.hpp:28)."""
+    with open(path, "rb") as f:
+        return parse_ppm(f.read())
+
+
+def huffman_text(text) -> list[tuple[int, int, int]]:
+    """generateHuffmanCode (Huffman.hpp:53) on an int text -> [(symbol, length, code)] in DHT order."""
+    t = np.ascontiguousarray(np.asarray(text, dtype=np.int32))
+    n = max(1, len(set(t.tolist())))
+    syms = np.zeros(n + 1, np.int32)
+    lens = np.zeros(n + 1, np.int32)
+    codes = np.zeros(n + 1, np.uint32)
+    k = ctypes.c_int()
+    _check(lib().jpge_huffman_text(_p(t), t.size, _p(syms), _p(lens), _p(codes), ctypes.byref(k)), "huffman_text")
+    return list(zip(syms[:k.value].tolist(), lens[:k.value].tolist(), codes[:k.value].tolist()))
+
+
+def huffman_table(counts, first):
+    """Byte-symbol table from counts/first-occurrence keys -> (bits[16], huffval list, code[256], len[256])."""
+    c = np.ascontiguousarray(counts, dtype=np.uint32)
+    f = np.ascontiguousarray(first, dtype=np.uint64)
+    bits = np.zeros(16, np.uint8)
+    hv = np.zeros(256, np.uint8)
+    code = np.zeros(256, np.uint32)
+    ln = np.zeros(256, np.uint8)
+    n = ctypes.c_int()
+    _check(lib().jpge_huffman_table(_p(c), _p(f), _p(bits), _p(hv), ctypes.byref(n), _p(code), _p(ln)),
+           "huffman_table")
+    return bits, hv[:n.value].tolist(), code, ln
+
+
+def arai_constants() -> tuple[np.ndarray, np.ndarray]:
+    a = np.zeros(5)
+    s = np.zeros(8)
+    lib().jpge_arai_constants(_p(a), _p(s))
+    return a, s
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().jpge_device_count(ctypes.byref(n))
+    return n.value
+
+
+def max_jpeg_bytes(width: int, height: int) -> int:
+    return int(lib().jpge_max_jpeg_bytes(width, height))
+
+
+class Encoder:
+    """One GPU context (jpge_open).  Host-array methods copy in/out; the `*_dev`
+    variants take device pointers (ints) for HBM-resident frames."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        _check(lib().jpge_open(int(device), ctypes.byref(self._ctx)), f"jpge_open({device})")
+        self.device = device
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().jpge_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self) -> ctypes.c_void_p:
+        return self._ctx
+
+    def set_timing(self, on: bool = True) -> None:
+        _check(lib().jpge_set_timing(self._ctx, int(on)), "set_timing")
+
+    def timing(self) -> dict:
+        t = Timing()
+        _check(lib().jpge_get_timing(self._ctx, ctypes.byref(t)), "get_timing")
+        return {"fdct": t.fdct, "dc_stats": t.dc_stats, "entropy": t.entropy, "total": t.total,
+                "fdct_sum": t.fdct_sum, "dc_stats_sum": t.dc_stats_sum, "entropy_sum": t.entropy_sum,
+                "frames": t.frames}
+
+    def reset_timing(self) -> None:
+        _check(lib().jpge_reset_timing(self._ctx), "reset_timing")
+
+    @staticmethod
+    def _tables(quality, qy, qc):
+        if qy is None or qc is None:
+            qy, qc = quality_tables(quality)
+        return np.ascontiguousarray(qy, np.uint8), np.ascontiguousarray(qc, np.uint8)
+
+    def encode(self, rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None) -> bytes:
+        """Image::writeJPEG (Image.cpp:831-976) on an (H, W, 3) uint8 frame -> .jpg bytes."""
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        h, w = rgb.shape[:2]
+        qy, qc = self._tables(quality, qy, qc)
+        out = np.empty(max_jpeg_bytes(w, h), np.uint8)
+        n = ctypes.c_size_t()
+        _check(lib().jpge_encode_rgb8(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(out),
+                                      out.size, ctypes.byref(n), 0), "encode")
+        return out[:n.value].tobytes()
+
+    def encode_batch_dev(self, frames: list[tuple[int, int, int, int]], outs: list[tuple[int, int]],
+                         quality: int = 50, maxval: int = 255) -> list[int]:
+        """Pipelined batch on device memory: frames = [(ptr, w, h, stride)], outs = [(ptr, cap)].
+        Returns the .jpg length of each frame (bytes stay in device memory)."""
+        qy, qc = self._tables(quality, None, None)
+        arr = (Frame * len(frames))()
+        for i, ((p, w, h, s), (o, cap)) in enumerate(zip(frames, outs)):
+            arr[i].rgb, arr[i].width, arr[i].height, arr[i].stride, arr[i].maxval = p, w, h, s, maxval
+            arr[i].out, arr[i].cap = o, cap
+        st = lib().jpge_encode_batch(self._ctx, arr, len(frames), _p(qy), _p(qc),
+                                     JPGE_DEVICE_INPUT | JPGE_DEVICE_OUTPUT)
+        _check(st, "encode_batch")
+        return [arr[i].len for i in range(len(frames))]
+
+    def encode_batch(self, frames: list[np.ndarray], quality: int = 50, maxval: int = 255) -> list[bytes]:
+        qy, qc = self._tables(quality, None, None)
+        frames = [np.ascontiguousarray(f, np.uint8) for f in frames]
+        outs = [np.empty(max_jpeg_bytes(f.shape[1], f.shape[0]), np.uint8) for f in frames]
+        arr = (Frame * len(frames))()
+        for i, (f, o) in enumerate(zip(frames, outs)):
+            arr[i].rgb, arr[i].width, arr[i].height = _p(f), f.shape[1], f.shape[0]
+            arr[i].stride, arr[i].maxval, arr[i].out, arr[i].cap = f.shape[1] * 3, maxval, _p(o), o.size
+        _check(lib().jpge_encode_batch(self._ctx, arr, len(frames), _p(qy), _p(qc), 0), "encode_batch")
+        return [outs[i][:arr[i].len].tobytes() for i in range(len(frames))]
+
+    def fdct_quant(self, rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None):
+        """Stage dump: quantised coefficients (before DC diff) -> (Y, Cb, Cr) arrays of shape
+        (nblocks, 64), blocks in raster order, natural order within a block."""
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        h, w = rgb.shape[:2]
+        W, H = (w + 15) // 16 * 16, (h + 15) // 16 * 16
+        y = np.zeros(((W // 8) * (H // 8), 64), np.int16)
+        cb = np.zeros(((W // 16) * (H // 16), 64), np.int16)
+        cr = np.zeros_like(cb)
+        qy, qc = self._tables(quality, qy, qc)
+        _check(lib().jpge_fdct_quant(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(y), _p(cb),
+                                     _p(cr), 0), "fdct_quant")
+        return y, cb, cr
+
+    def symbol_stats(self, rgb: np.ndarray, quality: int = 50, maxval: int = 255):
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        h, w = rgb.shape[:2]
+        qy, qc = self._tables(quality, None, None)
+        counts = np.zeros(1024, np.uint32)
+        first = np.zeros(1024, np.uint64)
+        _check(lib().jpge_symbol_stats(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(counts),
+                                       _p(first), 0), "symbol_stats")
+        return counts.reshape(4, 256), first.reshape(4, 256)
+
+
+def write_jpeg(path: str, ppm: PPM, quality: int = 50, device: int = 0) -> int:
+    """loadPPM + writeJPEG convenience; returns bytes written."""
+    with Encoder(device) as enc:
+        data = enc.encode(ppm.rgb, quality=quality, maxval=ppm.maxval)
+    with open(path, "wb") as f:
+        f.write(data)
+    return len(data)

@@ -1,0 +1,234 @@
+// extern "C" boundary (include/jpge.h) over jpge::Encoder and the host pieces.
+#include "jpge.h"
+
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "constants.hpp"
+#include "encoder.hpp"
+#include "host_io.hpp"
+#include "huffman.hpp"
+
+struct jpge_ctx {
+    std::unique_ptr<jpge::Encoder> enc;
+};
+
+namespace {
+jpge::FrameDesc frame(const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval) {
+    jpge::FrameDesc f;
+    f.rgb = rgb;
+    f.width = w;
+    f.height = h;
+    f.stride = stride;
+    f.maxval = maxval;
+    return f;
+}
+}  // namespace
+
+extern "C" {
+
+const char* jpge_strerror(int s) {
+    switch (s) {
+        case JPGE_OK: return "ok";
+        case JPGE_E_ARG: return "invalid argument";
+        case JPGE_E_NOSPACE: return "output buffer too small";
+        case JPGE_E_HIP: return "HIP runtime error";
+        case JPGE_E_NODEV: return "no such GPU device";
+        case JPGE_E_FORMAT: return "Only P3 and P6 format is supported!";
+        case JPGE_E_IO: return "failed to open file";
+        case JPGE_E_TRUNC: return "PPM sample data truncated";
+        case JPGE_E_RANGE: return "value out of range (maxval must be 1..255)";
+        case JPGE_E_TIMEOUT: return "device scan protocol timed out";
+        case JPGE_E_RCCL: return "RCCL error";
+        default: return "internal error";
+    }
+}
+
+int jpge_version(void) { return 100; }
+
+int jpge_device_count(int* n) {
+    if (!n) return JPGE_E_ARG;
+    if (hipGetDeviceCount(n) != hipSuccess) { *n = 0; return JPGE_E_NODEV; }
+    return JPGE_OK;
+}
+
+int jpge_open(int device, jpge_ctx** ctx) {
+    if (!ctx) return JPGE_E_ARG;
+    *ctx = nullptr;
+    std::unique_ptr<jpge_ctx> c(new (std::nothrow) jpge_ctx());
+    if (!c) return JPGE_E_INTERNAL;
+    int st = jpge::Encoder::open(device, c->enc);
+    if (st) return st;
+    *ctx = c.release();
+    return JPGE_OK;
+}
+
+int jpge_close(jpge_ctx* ctx) {
+    delete ctx;
+    return JPGE_OK;
+}
+
+int jpge_set_timing(jpge_ctx* ctx, int on) {
+    if (!ctx) return JPGE_E_ARG;
+    ctx->enc->set_timing(on != 0);
+    return JPGE_OK;
+}
+
+int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
+    if (!ctx || !t) return JPGE_E_ARG;
+    const auto& k = ctx->enc->times();
+    t->fdct = k.fdct;
+    t->dc_stats = k.dc_stats;
+    t->entropy = k.entropy;
+    t->total = k.total;
+    t->fdct_sum = k.fdct_sum;
+    t->dc_stats_sum = k.dc_stats_sum;
+    t->entropy_sum = k.entropy_sum;
+    t->frames = k.frames;
+    return JPGE_OK;
+}
+
+int jpge_reset_timing(jpge_ctx* ctx) {
+    if (!ctx) return JPGE_E_ARG;
+    ctx->enc->reset_timing();
+    return JPGE_OK;
+}
+
+size_t jpge_max_jpeg_bytes(uint32_t w, uint32_t h) { return jpge::Encoder::max_jpeg_bytes(w, h); }
+
+int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]) {
+    if (!qy || !qc || quality < 1 || quality > 100) return JPGE_E_ARG;
+    jpge::quality_tables(quality, qy, qc);
+    return JPGE_OK;
+}
+
+int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
+                     const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len,
+                     uint32_t flags) {
+    if (!ctx || !rgb || !qy || !qc || !out || !len) return JPGE_E_ARG;
+    jpge::FrameDesc f = frame(rgb, w, h, stride, maxval);
+    f.out = out;
+    f.cap = cap;
+    int st = ctx->enc->encode(f, qy, qc, flags);
+    *len = f.len;
+    return st;
+}
+
+int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
+                      uint32_t flags) {
+    if (!ctx || (!frames && n) || n < 0 || !qy || !qc) return JPGE_E_ARG;
+    std::vector<jpge::FrameDesc> fd(n);
+    for (int i = 0; i < n; ++i) {
+        fd[i] = frame(frames[i].rgb, frames[i].width, frames[i].height, frames[i].stride, frames[i].maxval);
+        fd[i].out = frames[i].out;
+        fd[i].cap = frames[i].cap;
+    }
+    int st = ctx->enc->encode_batch(fd.data(), n, qy, qc, flags);
+    for (int i = 0; i < n; ++i) {
+        frames[i].len = fd[i].len;
+        frames[i].status = fd[i].status;
+    }
+    return st;
+}
+
+int jpge_fdct_quant(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
+                    const uint8_t qy[64], const uint8_t qc[64], int16_t* cy, int16_t* ccb, int16_t* ccr,
+                    uint32_t flags) {
+    if (!ctx || !rgb || !qy || !qc || !cy || !ccb || !ccr) return JPGE_E_ARG;
+    return ctx->enc->fdct_quant(frame(rgb, w, h, stride, maxval), qy, qc, flags, cy, ccb, ccr);
+}
+
+int jpge_symbol_stats(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
+                      const uint8_t qy[64], const uint8_t qc[64], uint32_t counts[1024], uint64_t first[1024],
+                      uint32_t flags) {
+    if (!ctx || !rgb || !qy || !qc || !counts || !first) return JPGE_E_ARG;
+    return ctx->enc->symbol_stats(frame(rgb, w, h, stride, maxval), qy, qc, flags, counts, first);
+}
+
+int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], uint8_t bits[16],
+                       uint8_t huffval[256], int* nsym, uint32_t code[256], uint8_t len[256]) {
+    if (!counts || !first || !bits || !huffval || !nsym || !code || !len) return JPGE_E_ARG;
+    jpge::HuffTable t;
+    if (!jpge::build_table(counts, first, t)) return JPGE_E_ARG;
+    std::memcpy(bits, t.bits + 1, 16);
+    std::memcpy(huffval, t.huffval, 256);
+    *nsym = t.nsym;
+    std::memcpy(code, t.code, sizeof(t.code));
+    std::memcpy(len, t.len, sizeof(t.len));
+    return JPGE_OK;
+}
+
+int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t* codes, int* nsym) {
+    if (!text || !n || !syms || !lens || !codes || !nsym) return JPGE_E_ARG;
+    auto r = jpge::generateHuffmanCode(std::vector<int>(text, text + n));
+    int k = 0;
+    for (const auto& sc : r.first) {
+        syms[k] = sc.first;
+        lens[k] = sc.second.length;
+        codes[k] = sc.second.code;
+        ++k;
+    }
+    *nsym = k;
+    return JPGE_OK;
+}
+
+int jpge_ppm_info(const uint8_t* buf, size_t n, uint32_t* w, uint32_t* h, int* maxval) {
+    if (!buf || !w || !h || !maxval) return JPGE_E_ARG;
+    jpge::PpmImage img;
+    int st = jpge::parse_ppm(buf, n, img);
+    if (st && st != jpge::kErrTruncated && st != jpge::kErrRange) return st;
+    if (!img.width) return st ? st : JPGE_E_FORMAT;
+    *w = img.width;
+    *h = img.height;
+    *maxval = img.maxval;
+    return JPGE_OK;
+}
+
+int jpge_parse_ppm(const uint8_t* buf, size_t n, uint8_t* rgb, size_t cap, uint32_t* w, uint32_t* h, int* maxval) {
+    if (!buf || !rgb || !w || !h || !maxval) return JPGE_E_ARG;
+    jpge::PpmImage img;
+    int st = jpge::parse_ppm(buf, n, img);
+    if (st) return st;
+    if (img.rgb.size() > cap) return JPGE_E_NOSPACE;
+    std::memcpy(rgb, img.rgb.data(), img.rgb.size());
+    *w = img.width;
+    *h = img.height;
+    *maxval = img.maxval;
+    return JPGE_OK;
+}
+
+int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, int quality) {
+    if (!ctx || !ppm_path || !jpg_path) return JPGE_E_ARG;
+    jpge::PpmImage img;
+    int st = jpge::load_ppm_file(ppm_path, img);
+    if (st) return st;
+    uint8_t qy[64], qc[64];
+    if (quality < 1 || quality > 100) return JPGE_E_ARG;
+    jpge::quality_tables(quality, qy, qc);
+    std::vector<uint8_t> out(jpge::Encoder::max_jpeg_bytes(img.width, img.height));
+    size_t len = 0;
+    st = jpge_encode_rgb8(ctx, img.rgb.data(), img.width, img.height, 0, img.maxval, qy, qc, out.data(),
+                          out.size(), &len, 0);
+    if (st) return st;
+    std::ofstream f(jpg_path, std::ios::binary);
+    if (!f.is_open()) return JPGE_E_IO;
+    f.write(reinterpret_cast<const char*>(out.data()), (std::streamsize)len);
+    return f.good() ? JPGE_OK : JPGE_E_IO;
+}
+
+int jpge_synth_rgb8(uint64_t seed, uint32_t w, uint32_t h, int kind, uint8_t* out, size_t stride) {
+    if (!out || !w || !h || kind < 0 || kind > 2) return JPGE_E_ARG;
+    jpge::synth_rgb8(seed, w, h, kind, out, stride ? stride : (size_t)w * 3);
+    return JPGE_OK;
+}
+
+void jpge_arai_constants(double a[5], double s[8]) {
+    a[0] = jpge::kA1; a[1] = jpge::kA2; a[2] = jpge::kA3; a[3] = jpge::kA4; a[4] = jpge::kA5;
+    s[0] = jpge::kS0; s[1] = jpge::kS1; s[2] = jpge::kS2; s[3] = jpge::kS3;
+    s[4] = jpge::kS4; s[5] = jpge::kS5; s[6] = jpge::kS6; s[7] = jpge::kS7;
+}
+
+}  // extern "C"

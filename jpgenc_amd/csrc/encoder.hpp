@@ -1,0 +1,76 @@
+// Host orchestration of the GPU encode path: one Encoder = one HIP device, a
+// small ring of frame slots (each with its own stream and workspace), and the
+// per-image Huffman-table build between the statistics kernels and the entropy
+// kernel.  This is the engine behind the C ABI (include/jpge.h).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+#include "host_io.hpp"
+#include "huffman.hpp"
+#include "kernels.hpp"
+
+namespace jpge {
+
+constexpr uint32_t kFlagDeviceInput = 1u;
+constexpr uint32_t kFlagDeviceOutput = 2u;
+
+struct FrameDesc {
+    const uint8_t* rgb = nullptr;
+    uint32_t width = 0, height = 0;
+    size_t stride = 0;  // bytes per input row (0 = width*3)
+    int maxval = 255;
+    uint8_t* out = nullptr;
+    size_t cap = 0;
+    size_t len = 0;
+    int status = 0;
+};
+
+struct KernelTimes {  // milliseconds of the last timed frame (HIP events on the slot stream)
+    float fdct = 0, dc_stats = 0, entropy = 0, total = 0;
+    double fdct_sum = 0, dc_stats_sum = 0, entropy_sum = 0;  // accumulated since reset
+    uint64_t frames = 0;
+};
+
+class Encoder {
+  public:
+    static int open(int device, std::unique_ptr<Encoder>& out);
+    ~Encoder();
+
+    int encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
+    int encode_batch(FrameDesc* frames, int n, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
+
+    // Stage entry: quantised coefficients (before DC differencing), per component
+    // in block raster order, 64 natural-order values per block (host buffers).
+    int fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
+                   int16_t* y, int16_t* cb, int16_t* cr);
+    // Stage entry: the four symbol histograms and first-occurrence keys.
+    int symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
+                     uint32_t counts[1024], uint64_t first[1024]);
+
+    void set_timing(bool on) { timing_ = on; }
+    void reset_timing() { times_ = KernelTimes(); }
+    const KernelTimes& times() const { return times_; }
+    int device() const { return device_; }
+    static size_t max_jpeg_bytes(uint32_t w, uint32_t h);
+
+  private:
+    struct Slot;
+    Encoder() = default;
+    int ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap);
+    int phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
+    int phase2(Slot& s, const FrameDesc& f, uint32_t flags);
+    int finish(Slot& s, FrameDesc& f, uint32_t flags);
+    int upload_tables(Slot& s, const uint8_t qy[64], const uint8_t qc[64]);
+
+    int device_ = 0;
+    bool timing_ = false;
+    KernelTimes times_;
+    std::vector<std::unique_ptr<Slot>> slots_;
+};
+
+}  // namespace jpge

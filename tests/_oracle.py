@@ -1,0 +1,145 @@
+"""ctypes access to the TEST-ONLY oracle (oracle/build/liborc.so) and, when it was
+built in this container, the reference's own Huffman/Bitstream code
+(oracle/_ref/libref.so).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg use this module."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORC_PATH = os.path.join(ROOT, "oracle", "build", "liborc.so")
+REF_PATH = os.path.join(ROOT, "oracle", "_ref", "libref.so")
+
+_orc = None
+_ref = None
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def orc() -> ctypes.CDLL:
+    global _orc
+    if _orc is None:
+        if not os.path.exists(ORC_PATH):
+            raise ImportError(f"{ORC_PATH} missing: run `make oracle`")
+        L = ctypes.CDLL(ORC_PATH)
+        vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
+        L.orc_quality_tables.argtypes = [i32, vp, vp]
+        L.orc_arai_constants.argtypes = [vp, vp, vp]
+        L.orc_dct_arai.argtypes = [vp, vp]
+        L.orc_quantize.argtypes = [vp, vp, vp]
+        L.orc_ycc.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+        L.orc_zigzag_to_natural.argtypes = [i32]
+        L.orc_subsample420m.argtypes = [vp, i32, i32, vp]
+        L.orc_category.argtypes = [i32, vp]
+        L.orc_rle_block.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.orc_huffman.argtypes = [vp, i32, vp, vp, vp]
+        L.orc_pack_bits.restype = i64
+        L.orc_pack_bits.argtypes = [vp, vp, i32, i32, vp, i64, vp]
+        L.orc_parse_ppm.argtypes = [vp, sz, vp, vp, vp, vp, sz]
+        L.orc_stage_coeffs.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
+        L.orc_stage_ycc.argtypes = [vp, i32, i32, i32, vp, vp, vp]
+        L.orc_stage_hist.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp]
+        L.orc_encode_rgb.restype = i64
+        L.orc_encode_rgb.argtypes = [vp, i32, i32, i32, vp, vp, vp, i64]
+        L.orc_set_threads.argtypes = [i32]
+        _orc = L
+    return _orc
+
+
+def ref() -> ctypes.CDLL | None:
+    """The reference's own code, or None when it could not be built here."""
+    global _ref
+    if _ref is None and os.path.exists(REF_PATH):
+        L = ctypes.CDLL(REF_PATH)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        L.ref_huffman.argtypes = [vp, i32, vp, vp, vp]
+        L.ref_package_merge.argtypes = [vp, vp, i32, i32, vp, vp]
+        L.ref_pack_bits.restype = i64
+        L.ref_pack_bits.argtypes = [vp, vp, vp, i32, i32, vp, i64, vp]
+        _ref = L
+    return _ref
+
+
+def quality_tables(q: int):
+    qy = np.zeros(64, np.uint8)
+    qc = np.zeros(64, np.uint8)
+    orc().orc_quality_tables(q, _p(qy), _p(qc))
+    return qy, qc
+
+
+def huffman(text, lib=None, fn="orc_huffman"):
+    t = np.ascontiguousarray(np.asarray(text, np.int32))
+    n = len(t) + 1
+    s = np.zeros(n, np.int32)
+    ln = np.zeros(n, np.int32)
+    c = np.zeros(n, np.uint32)
+    L = lib if lib is not None else orc()
+    k = getattr(L, fn)(_p(t), t.size, _p(s), _p(ln), _p(c))
+    return list(zip(s[:k].tolist(), ln[:k].tolist(), c[:k].tolist()))
+
+
+def encode(rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None) -> bytes:
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    if qy is None:
+        qy, qc = quality_tables(quality)
+    cap = 4096 + ((w + 15) // 16) * ((h + 15) // 16) * 6 * 420
+    out = np.empty(cap, np.uint8)
+    n = orc().orc_encode_rgb(_p(rgb), w, h, maxval, _p(np.ascontiguousarray(qy, np.uint8)),
+                             _p(np.ascontiguousarray(qc, np.uint8)), _p(out), cap)
+    if n < 0:
+        raise RuntimeError(f"oracle encode failed: {n}")
+    return out[:n].tobytes()
+
+
+def stage_coeffs(rgb: np.ndarray, quality: int = 50, maxval: int = 255):
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    W, H = (w + 15) // 16 * 16, (h + 15) // 16 * 16
+    qy, qc = quality_tables(quality)
+    y = np.zeros(((W // 8) * (H // 8), 64), np.int16)
+    cb = np.zeros(((W // 16) * (H // 16), 64), np.int16)
+    cr = np.zeros_like(cb)
+    orc().orc_stage_coeffs(_p(rgb), w, h, maxval, _p(qy), _p(qc), _p(y), _p(cb), _p(cr))
+    return y, cb, cr
+
+
+def stage_hist(rgb: np.ndarray, quality: int = 50, maxval: int = 255):
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    qy, qc = quality_tables(quality)
+    counts = np.zeros(1024, np.uint32)
+    first = np.zeros(1024, np.int64)
+    orc().orc_stage_hist(_p(rgb), w, h, maxval, _p(qy), _p(qc), _p(counts), _p(first))
+    return counts.reshape(4, 256), first.reshape(4, 256)
+
+
+def parse_ppm(data: bytes):
+    buf = np.frombuffer(data, np.uint8)
+    w, h, mv = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    st = orc().orc_parse_ppm(_p(buf), buf.size, ctypes.byref(w), ctypes.byref(h), ctypes.byref(mv), None, 0)
+    if st:
+        return st, None, None
+    samples = np.zeros(w.value * h.value * 3, np.int32)
+    st = orc().orc_parse_ppm(_p(buf), buf.size, ctypes.byref(w), ctypes.byref(h), ctypes.byref(mv), _p(samples),
+                             samples.size)
+    return st, samples.reshape(h.value, w.value, 3), mv.value
+
+
+def pack_bits(vals, nbits, do_fill=True, modes=None, lib=None):
+    v = np.ascontiguousarray(vals, np.uint32)
+    nb = np.ascontiguousarray(nbits, np.int32)
+    cap = int(nb.sum()) // 4 + 64
+    out = np.empty(cap, np.uint8)
+    raw = ctypes.c_int64()
+    if lib is None:
+        n = orc().orc_pack_bits(_p(v), _p(nb), v.size, int(do_fill), _p(out), cap, ctypes.byref(raw))
+    else:
+        m = np.ascontiguousarray(modes if modes is not None else np.zeros(v.size), np.int32)
+        n = lib.ref_pack_bits(_p(v), _p(nb), _p(m), v.size, int(do_fill), _p(out), cap, ctypes.byref(raw))
+    return out[:n].tobytes(), raw.value

@@ -1,0 +1,132 @@
+"""GPU parity: the HIP path (libjpge.so through the C ABI) against the oracle,
+bit-exact — quantised coefficients, symbol statistics and whole .jpg files."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+import _oracle
+import jpgenc_amd as J
+
+pytestmark = pytest.mark.gpu
+
+
+def _scaled(rgb, maxval):
+    return (rgb.astype(np.uint32) * maxval // 255).astype(np.uint8)
+
+
+def _ppm_files():
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ppm")
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".ppm"))
+
+
+@pytest.mark.parametrize("path", _ppm_files(), ids=lambda p: os.path.basename(p))
+@pytest.mark.parametrize("quality", [50, 90])
+def test_reference_images_bit_exact(encoder, path, quality):
+    img = J.load_ppm(path)
+    got = encoder.encode(img.rgb, quality=quality, maxval=img.maxval)
+    want = _oracle.encode(img.rgb, quality, img.maxval)
+    assert got == want
+
+
+SIZES = [(1, 1), (4, 4), (8, 8), (16, 16), (17, 33), (26, 19), (64, 64), (100, 60), (200, 136), (333, 211),
+         (512, 512)]
+
+
+@pytest.mark.parametrize("w,h", SIZES)
+@pytest.mark.parametrize("quality", [50, 90, 100])
+def test_synthetic_bit_exact(encoder, w, h, quality):
+    rgb = J.synth_rgb8(w * 1000 + h, w, h)
+    assert encoder.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
+
+
+@pytest.mark.parametrize("kind", [1, 2])
+@pytest.mark.parametrize("quality", [10, 50, 100])
+def test_stress_kinds_bit_exact(encoder, kind, quality):
+    # kind 1 = random bytes (long codes, many 0xFF), kind 2 = flat (one-symbol tables)
+    rgb = J.synth_rgb8(77 + kind, 160, 96, kind=kind)
+    assert encoder.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
+
+
+@pytest.mark.parametrize("maxval", [1, 15, 100, 254])
+def test_maxval_scaling_bit_exact(encoder, maxval):
+    rgb = _scaled(J.synth_rgb8(5, 120, 72), maxval)
+    for q in (50, 90):
+        assert encoder.encode(rgb, quality=q, maxval=maxval) == _oracle.encode(rgb, q, maxval)
+
+
+@pytest.mark.parametrize("w,h,maxval", [(64, 48, 255), (130, 70, 255), (512, 512, 255), (96, 64, 100)])
+def test_stage_coefficients_bit_exact(encoder, w, h, maxval):
+    rgb = _scaled(J.synth_rgb8(w + h, w, h), maxval)
+    for q in (50, 90, 100):
+        gy, gcb, gcr = encoder.fdct_quant(rgb, quality=q, maxval=maxval)
+        oy, ocb, ocr = _oracle.stage_coeffs(rgb, q, maxval)
+        assert np.array_equal(gy, oy) and np.array_equal(gcb, ocb) and np.array_equal(gcr, ocr)
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (200, 136), (512, 512)])
+def test_symbol_statistics(encoder, w, h):
+    rgb = J.synth_rgb8(w * h, w, h)
+    for q in (50, 90):
+        counts, first = encoder.symbol_stats(rgb, quality=q)
+        ocounts, ofirst = _oracle.stage_hist(rgb, q)
+        assert np.array_equal(counts, ocounts)
+        for t in range(4):
+            present = np.nonzero(ocounts[t])[0]
+            # first-occurrence ORDER is what the table build consumes
+            assert list(present[np.argsort(first[t][present], kind="stable")]) == \
+                list(present[np.argsort(ofirst[t][present], kind="stable")])
+
+
+def test_config2_1080p_q90_coefficients_and_file(encoder):
+    rgb = J.synth_rgb8(2, 1920, 1080)
+    gy, gcb, gcr = encoder.fdct_quant(rgb, quality=90)
+    oy, ocb, ocr = _oracle.stage_coeffs(rgb, 90)
+    assert np.array_equal(gy, oy) and np.array_equal(gcb, ocb) and np.array_equal(gcr, ocr)
+    assert encoder.encode(rgb, quality=90) == _oracle.encode(rgb, 90)
+
+
+@pytest.mark.parametrize("quality", [50, 90, 100])
+def test_config3_4k_bit_exact(encoder, quality):
+    rgb = J.synth_rgb8(3, 3840, 2160)
+    assert encoder.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
+
+
+def test_batch_matches_single(encoder):
+    frames = [J.synth_rgb8(1000 + i, 320 + 16 * (i % 3), 200 + 8 * i) for i in range(7)]
+    outs = encoder.encode_batch(frames, quality=90)
+    for f, o in zip(frames, outs):
+        assert o == encoder.encode(f, quality=90)
+        assert o == _oracle.encode(f, 90)
+
+
+def test_output_decodes(encoder):
+    Image = pytest.importorskip("PIL.Image")
+    rgb = J.synth_rgb8(42, 640, 480)
+    data = encoder.encode(rgb, quality=90)
+    im = Image.open(io.BytesIO(data))
+    im.load()
+    assert im.size == (640, 480)
+    dec = np.asarray(im.convert("RGB"), np.float64)
+    assert 10 * np.log10(255 ** 2 / np.mean((dec - rgb) ** 2)) > 28
+
+
+def test_deterministic_repeat(encoder):
+    rgb = J.synth_rgb8(9, 1280, 720, kind=1)
+    a = encoder.encode(rgb, quality=95)
+    b = encoder.encode(rgb, quality=95)
+    assert a == b
+
+
+def test_facade_cli_roundtrip(tmp_path):
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "tests", "golden", "ppm", "tester_RGB_26x19.ppm")
+    out = tmp_path / "o.jpg"
+    r = subprocess.run([os.path.join(root, "jpgenc_amd", "bin", "jpgenc"), src, str(out)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Processing image size: 26x19" in r.stdout and "Encoding duration:" in r.stdout
+    img = J.load_ppm(src)
+    assert out.read_bytes() == _oracle.encode(img.rgb, 50, img.maxval)
