@@ -55,7 +55,6 @@ struct Encoder::Slot {
     uint8_t* d_in = nullptr;
     int16_t* d_coef = nullptr;
     uint64_t* d_mask = nullptr;
-    int16_t* d_dc = nullptr;
     uint8_t* d_ctl = nullptr;
     uint8_t* d_out = nullptr;
     double* d_q = nullptr;
@@ -77,7 +76,7 @@ struct Encoder::Slot {
     uint8_t qy[64], qc[64];
 
     ~Slot() {
-        hipFree(d_in); hipFree(d_coef); hipFree(d_mask); hipFree(d_dc); hipFree(d_ctl);
+        hipFree(d_in); hipFree(d_coef); hipFree(d_mask); hipFree(d_ctl);
         hipFree(d_out); hipFree(d_q); hipFree(d_tab);
         hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_hdr); hipHostFree(h_result); hipHostFree(h_q);
         for (auto& e : ev) if (e) hipEventDestroy(e);
@@ -125,11 +124,10 @@ Encoder::~Encoder() {
 int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap) {
     const size_t nmcu = g.nmcu();
     if (nmcu > s.cap_mcu) {
-        hipFree(s.d_coef); hipFree(s.d_mask); hipFree(s.d_dc);
-        s.d_coef = nullptr; s.d_mask = nullptr; s.d_dc = nullptr; s.cap_mcu = 0;
+        hipFree(s.d_coef); hipFree(s.d_mask);
+        s.d_coef = nullptr; s.d_mask = nullptr; s.cap_mcu = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_coef, nmcu * 768));
         JPGE_HIP(hipMalloc((void**)&s.d_mask, nmcu * 6 * 8));
-        JPGE_HIP(hipMalloc((void**)&s.d_dc, align_up(nmcu * 12, 256)));
         s.cap_mcu = nmcu;
     }
     const CtlLayout L(entropy_tiles(g));
@@ -210,15 +208,16 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     a.maxval = f.maxval;
     a.qtab = s.d_q;
     a.coef = s.d_coef;
-    a.mask = s.d_mask;
-    a.dc = s.d_dc;
-    a.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
-    a.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
-    a.do_hist = 1;
+    StatsArgs st2;
+    st2.coef = s.d_coef;
+    st2.mask = s.d_mask;
+    st2.g = g;
+    st2.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
+    st2.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
     JPGE_HIP(launch_fdct(a, s.stream));
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
-    JPGE_HIP(launch_dc_stats(s.d_dc, g, a.hist, s.stream));
+    JPGE_HIP(launch_stats(st2, s.stream));
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[2], s.stream));
     JPGE_HIP(hipMemcpyAsync(s.h_hist->cnt, s.d_ctl + L.cnt, sizeof(s.h_hist->cnt), hipMemcpyDeviceToHost, s.stream));
     JPGE_HIP(hipMemcpyAsync(s.h_hist->key, s.d_ctl + L.key, sizeof(s.h_hist->key), hipMemcpyDeviceToHost, s.stream));
@@ -258,7 +257,6 @@ int Encoder::phase2(Slot& s, const FrameDesc& f, uint32_t flags) {
     EntropyArgs e;
     e.coef = s.d_coef;
     e.mask = s.d_mask;
-    e.dc = s.d_dc;
     e.g = s.g;
     e.tables = s.d_tab;
     e.out = s.out_dev;
@@ -351,7 +349,7 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
             int16_t* dst;
             if (k < 4) dst = y + ((size_t)(2 * mr + (k >> 1)) * ybw + 2 * mc + (k & 1)) * 64;
             else dst = (k == 4 ? cb : cr) + ((size_t)mr * cbw + mc) * 64;
-            for (int i = 0; i < 64; ++i) dst[kZigzagToNatural[i]] = src[i];
+            for (int i = 0; i < 64; ++i) dst[i] = src[i];
         }
     }
     return kOk;

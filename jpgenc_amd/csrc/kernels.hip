@@ -1,25 +1,25 @@
 // jpge HIP kernels for gfx950 (MI355X, CDNA4, wave64).
 //
-//   K1 fdct_kernel     RGB8 -> YCbCr -> 4:2:0 (S420_m) -> Arai FDCT (fp64) ->
-//                      quantise -> int16 zig-zag coefficients, AC non-zero masks,
-//                      DC values, and the Y-AC / C-AC symbol histograms with
-//                      first-occurrence keys.  One wavefront owns a tile of 4 MCUs
-//                      (64x16 px); the tile is staged in LDS for the column and
-//                      row passes.  Reference: Image.cpp:112-147, 198-235,
-//                      540-636, Dct.hpp:47-215, Coding.hpp:84-97.
-//   K2 dc_stats_kernel DC difference chain (Y in MCU order, Cb/Cr in block
-//                      order, Image.cpp:638-678) -> Y-DC / C-DC histograms.
-//   K3 entropy_kernel  DC diff + zig-zag RLE + category coding (Coding.hpp:
-//                      148-283) + Huffman emission (Image.cpp:737-829) + MCU
-//                      interleave (:957-968) + 1-fill + 0xFF00 stuffing
-//                      (BitstreamGeneric.hpp:213-248), as ONE kernel with two
-//                      decoupled look-back scans (bit offsets, then stuffed-byte
-//                      offsets).  One thread owns one 8x8 block.
+//   K1 fdct_kernel   RGB8 -> YCbCr -> 4:2:0 (S420_m) -> Arai FDCT (fp64) -> quantise
+//                    -> int16 coefficients (natural order, MCU-interleaved blocks).
+//                    One wavefront owns a tile of 4 MCUs (64x16 px) staged in LDS for
+//                    the column pass, the transpose and the row pass; each lane stores
+//                    one 16-byte row of a block straight from registers.
+//                    Reference: Image.cpp:112-147, 198-235, 540-636; Dct.hpp:47-215;
+//                    Coding.hpp:84-97.
+//   K2 stats_kernel  DC difference chain (Image.cpp:638-678) + zig-zag RLE + category
+//                    coding (Coding.hpp:148-283) -> the four symbol histograms of
+//                    writeJPEG's "texts" (Image.cpp:888-906) with first-occurrence keys;
+//                    also the per-block AC non-zero masks for K3.  Thread = block.
+//   K3 entropy_kernel Huffman emission (Image.cpp:737-829) in MCU interleave order
+//                    (:957-968), 1-fill and 0xFF00 stuffing (BitstreamGeneric.hpp:
+//                    213-248) in ONE pass with two decoupled look-back scans (bit
+//                    offsets, then stuffed-byte offsets).  Thread = block.
 //
-// Bit-exactness: every fp64 operation of the reference is reproduced in order
-// with no contraction (this file is compiled with -ffp-contract=off and the
-// pragma below); colour conversion of 8-bit input uses FMA chains only where the
-// result is provably exact (all terms are multiples of 2^-27 well inside 53 bits).
+// Bit-exactness: every fp64 operation of the reference is reproduced in order with
+// no contraction (compiled with -ffp-contract=off plus the pragma below); the colour
+// conversion of 8-bit input uses FMA chains only where every partial result is exact
+// (all terms are multiples of 2^-27 far inside 53 bits).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -37,17 +37,23 @@ constexpr double kYr = (double).299f, kYg = (double).587f, kYb = (double).114f;
 constexpr double kCbR = (double)-.1687f, kCbG = (double)-.3312f, kCbB = (double).5f;
 constexpr double kCrR = (double).5f, kCrG = (double)-.4186f, kCrB = (double)-.0813f;
 
-__constant__ uint8_t kNaturalToZigzag[64] = {
+// natural (row-major) index -> zig-zag position (inverse of Coding.hpp:57-81)
+__constant__ uint8_t kNatToZz[64] = {
     0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42,
     3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24, 31, 40, 44, 53,
     10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
-// Orders LDS traffic between lanes of ONE wavefront (DS ops of a wave execute
-// in order; this only stops the compiler from moving them).
+// Orders LDS traffic between lanes of ONE wavefront (a wave's DS ops execute in
+// order; this stops the compiler from moving them across the point).
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int category(int v) {  // getCategoryAndCode, Coding.hpp:197-230
+    const int av = v < 0 ? -v : v;
+    return av ? 32 - __builtin_clz((unsigned)av) : 0;
 }
 
 // One 8-point Arai pass, Dct.hpp:62-131 (same op order for both passes).
@@ -71,30 +77,27 @@ __device__ __forceinline__ void arai8(const double x[8], double o[8]) {
 // division, then round half away from zero.
 __device__ __forceinline__ int quant1(double d, double q) { return (int)round(d / q); }
 
-// ---------------------------------------------------------------------------
-// K1
-// ---------------------------------------------------------------------------
-constexpr int kK1Threads = 256;             // 4 waves, one tile (4 MCUs) each
-constexpr int kRgbPitch = 66;               // u32 per staged pixel row (bank spread)
-constexpr int kTmpBlock = 72;               // doubles per transposition block (9-double rows)
+// ===========================================================================
+// K1 — colour + 4:2:0 + FDCT + quantise
+// ===========================================================================
+constexpr int kK1Threads = 256;  // 4 waves, one 4-MCU tile each
+constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
+constexpr int kTmpBlock = 72;    // doubles per transpose block (rows of 9 doubles)
 constexpr int kTmpRow = 9;
 
 struct K1WaveLds {
-    uint32_t rgbx[16 * kRgbPitch];          // packed R | G<<8 | B<<16
-    double tmp[8 * kTmpBlock];              // pass-1 output, transposed
-    int16_t zz[24 * 64];                    // quantised, zig-zag, MCU-interleaved
+    uint32_t rgbx[16 * kRgbPitch];  // packed R | G<<8 | B<<16
+    double tmp[8 * kTmpBlock];      // pass-1 output, transposed
 };
 struct K1Lds {
     K1WaveLds w[4];
     double q[128];
-    uint32_t hcnt[2][256];                  // Y-AC, C-AC
-    unsigned long long hkey[2][256];        // ~first key (max == earliest)
 };
 
-__device__ __forceinline__ void ycc_exact_y(uint32_t p, double& y) {
+__device__ __forceinline__ double ycc_exact_y(uint32_t p) {
     const double r = (double)(p & 0xFF), g = (double)((p >> 8) & 0xFF), b = (double)(p >> 16);
-    // (0 + ((.299 r + .587 g) + .114 b)) - 128 ; every partial result is exact.
-    y = __builtin_fma(kYb, b, __builtin_fma(kYg, g, __builtin_fma(kYr, r, -128.0)));
+    // (0 + ((.299 r + .587 g) + .114 b)) - 128 : every partial result is exact
+    return __builtin_fma(kYb, b, __builtin_fma(kYg, g, __builtin_fma(kYr, r, -128.0)));
 }
 
 __device__ __forceinline__ double ycc_ref_y(uint32_t p, double scale) {
@@ -112,83 +115,69 @@ __device__ __forceinline__ double ycc_ref_c(uint32_t p, double scale, double kr,
 template <bool kExact>
 __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
     __shared__ K1Lds lds;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     K1WaveLds& W = lds.w[wv];
-
     for (int i = tid; i < 128; i += kK1Threads) lds.q[i] = a.qtab[i];
-    for (int i = tid; i < 512; i += kK1Threads) {
-        (&lds.hcnt[0][0])[i] = 0;
-        (&lds.hkey[0][0])[i] = 0;
-    }
     __syncthreads();
 
-    const uint32_t mw = a.g.mw, mh = a.g.mh;
+    const uint32_t mw = a.g.mw;
     const uint32_t tiles_per_row = (mw + 3) / 4;
-    const uint32_t ntiles = tiles_per_row * mh;
+    const uint32_t ntiles = tiles_per_row * a.g.mh;
     const uint32_t nwaves = gridDim.x * 4;
     const double scale = 255.0 / (double)a.maxval;  // Image.cpp:465
+    const bool aligned = (((uintptr_t)a.rgb | a.stride) & 15) == 0;
+    const int r16 = lane >> 2, c16 = lane & 3;  // staging: lane -> (pixel row, 16-px chunk)
+    const int b8 = lane >> 3, j = lane & 7;     // DCT: lane -> (block of the round, column)
 
     for (uint32_t t = blockIdx.x * 4 + wv; t < ntiles; t += nwaves) {
         const uint32_t mrow = t / tiles_per_row;
         const uint32_t mcol0 = (t % tiles_per_row) * 4;
         const int nvalid = (int)min(4u, mw - mcol0);
-        const uint32_t x0 = mcol0 * 16, y0 = mrow * 16;
+        const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
 
-        // ---- stage RGB: lane -> (row lane/4, 16 px chunk lane%4) ----
-        {
-            const int r = lane >> 2, c = lane & 3;
-            const uint32_t y = y0 + r, xs = x0 + c * 16;
-            uint32_t px[16];
-            const bool fast = (y < a.g.height) && (xs + 16 <= a.g.width) &&
-                              (((uintptr_t)a.rgb | a.stride) & 15) == 0;
-            if (fast) {
-                const uint4* src = reinterpret_cast<const uint4*>(a.rgb + (uint64_t)y * a.stride + (uint64_t)xs * 3);
-                uint4 v0 = src[0], v1 = src[1], v2 = src[2];
-                uint32_t wd[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+        // ---- stage 16 px per lane as packed u32 ----
+        uint32_t px[16];
+        if (aligned && y < a.g.height && xs + 16 <= a.g.width) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.rgb + (uint64_t)y * a.stride + (uint64_t)xs * 3);
+            const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+            const uint32_t wd[13] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, 0u};
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    // bytes 3i..3i+2 of the 48-byte run
-                    const int b0 = 3 * i;
-                    const uint64_t pair = ((uint64_t)wd[(b0 >> 2) + ((b0 >> 2) < 11 ? 1 : 0)] << 32) | wd[b0 >> 2];
-                    px[i] = (uint32_t)(pair >> (8 * (b0 & 3))) & 0xFFFFFFu;
-                }
-            } else {
-                // edge replication (Image.cpp:498-531) as clamped addressing
-                const uint32_t sy = min(y, a.g.height - 1);
-                for (int i = 0; i < 16; ++i) {
-                    const uint32_t sx = min(xs + i, a.g.width - 1);
-                    const uint8_t* p = a.rgb + (uint64_t)sy * a.stride + (uint64_t)sx * 3;
-                    px[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-                }
+            for (int i = 0; i < 16; ++i) {
+                const int b0 = 3 * i, d = b0 >> 2, sh = 8 * (b0 & 3);
+                px[i] = (sh ? __builtin_amdgcn_alignbit(wd[d + 1], wd[d], sh) : wd[d]) & 0xFFFFFFu;
             }
-            uint32_t* dst = &W.rgbx[r * kRgbPitch + c * 16];
-#pragma unroll
-            for (int i = 0; i < 16; i += 2)
-                *reinterpret_cast<uint2*>(dst + i) = make_uint2(px[i], px[i + 1]);
+        } else {  // right/bottom edge replication (Image.cpp:498-531) as clamped addressing
+            const uint32_t sy = min(y, a.g.height - 1);
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t sx = min(xs + i, a.g.width - 1);
+                const uint8_t* p = a.rgb + (uint64_t)sy * a.stride + (uint64_t)sx * 3;
+                px[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+            }
         }
+        uint32_t* dst = &W.rgbx[r16 * kRgbPitch + c16 * 16];
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) *reinterpret_cast<uint2*>(dst + i) = make_uint2(px[i], px[i + 1]);
         wave_lds_sync();
 
-        // ---- three rounds of 8 blocks x 8 columns: Y, Y, then Cb/Cr ----
-        const int b8 = lane >> 3, j = lane & 7;
+        // ---- rounds: Y blocks 0-7, Y blocks 8-15, then Cb x4 + Cr x4 ----
 #pragma unroll 1
         for (int round = 0; round < 3; ++round) {
             double x[8];
-            int slot, qbase;
+            int m, slot, qb;
             if (round < 2) {
-                const int yb = round * 8 + b8, m = yb >> 2, sub = yb & 3;
+                const int yb = round * 8 + b8, sub = yb & 3;
+                m = yb >> 2;
                 const int col = m * 16 + (sub & 1) * 8 + j, row0 = (sub >> 1) * 8;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const uint32_t p = W.rgbx[(row0 + i) * kRgbPitch + col];
-                    if (kExact) ycc_exact_y(p, x[i]);
-                    else x[i] = ycc_ref_y(p, scale);
+                    x[i] = kExact ? ycc_exact_y(p) : ycc_ref_y(p, scale);
                 }
-                slot = m * 6 + sub;
-                qbase = 0;
+                slot = sub;
+                qb = 0;
             } else {
-                const int comp = b8 >> 2, m = b8 & 3;
+                const int comp = b8 >> 2;
+                m = b8 & 3;
                 const double kr = comp ? kCrR : kCbR, kg = comp ? kCrG : kCbG, kb = comp ? kCrB : kCbB;
                 const int col = m * 16 + 2 * j;
 #pragma unroll
@@ -196,32 +185,28 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
                     const uint2 t0 = *reinterpret_cast<const uint2*>(&W.rgbx[(2 * i) * kRgbPitch + col]);
                     const uint2 t1 = *reinterpret_cast<const uint2*>(&W.rgbx[(2 * i + 1) * kRgbPitch + col]);
                     if (kExact) {
-                        // ((a+b)+(c+d))/4 of exact per-pixel values == exact value of
-                        // the channel sums; every partial is exact.
-                        const uint32_t s = (t0.x & 0xFF00FFu) + (t0.y & 0xFF00FFu) + (t1.x & 0xFF00FFu) + (t1.y & 0xFF00FFu);
+                        // ((a+b)+(c+d))/4 of the exact per-pixel values equals the exact
+                        // value of the channel sums
+                        const uint32_t s = (t0.x & 0xFF00FFu) + (t0.y & 0xFF00FFu) + (t1.x & 0xFF00FFu) +
+                                           (t1.y & 0xFF00FFu);
                         const double sr = (double)(s & 0xFFFF), sb = (double)(s >> 16);
                         const double sg = (double)(((t0.x >> 8) & 0xFF) + ((t0.y >> 8) & 0xFF) +
                                                    ((t1.x >> 8) & 0xFF) + ((t1.y >> 8) & 0xFF));
                         x[i] = __builtin_fma(kb, sb, __builtin_fma(kg, sg, kr * sr)) * 0.25;
                     } else {
-                        // subsample(S420_m), Image.cpp:207-224: ((a + b) + (c + d)) / 4
-                        const double va = ycc_ref_c(t0.x, scale, kr, kg, kb);
-                        const double vb = ycc_ref_c(t0.y, scale, kr, kg, kb);
-                        const double vc = ycc_ref_c(t1.x, scale, kr, kg, kb);
-                        const double vd = ycc_ref_c(t1.y, scale, kr, kg, kb);
-                        double top = 0.0;
-                        top += va;
-                        top += vb;
-                        double bot = 0.0;
-                        bot += vc;
-                        bot += vd;
+                        // subsample(S420_m), Image.cpp:207-224: ((0+a+b) + (0+c+d)) / 4
+                        double top = 0.0, bot = 0.0;
+                        top += ycc_ref_c(t0.x, scale, kr, kg, kb);
+                        top += ycc_ref_c(t0.y, scale, kr, kg, kb);
+                        bot += ycc_ref_c(t1.x, scale, kr, kg, kb);
+                        bot += ycc_ref_c(t1.y, scale, kr, kg, kb);
                         x[i] = (top + bot) / 4;
                     }
                 }
-                slot = m * 6 + 4 + comp;
-                qbase = 64;
+                slot = 4 + comp;
+                qb = 64;
             }
-            // pass 1 over the column, result written transposed (Dct.hpp:124-131)
+            // column pass, written transposed (Dct.hpp:124-131); row pass
             double o[8];
             arai8(x, o);
             double* tb = &W.tmp[b8 * kTmpBlock];
@@ -231,145 +216,172 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) x[i] = tb[i * kTmpRow + j];
             arai8(x, o);  // o[u] = y(j, u)
-            int16_t* zb = &W.zz[slot * 64];
+            int qv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                zb[kNaturalToZigzag[j * 8 + u]] = (int16_t)quant1(o[u], lds.q[qbase + j * 8 + u]);
+            for (int u = 0; u < 8; ++u) qv[u] = quant1(o[u], lds.q[qb + j * 8 + u]);
+            if (m < nvalid) {
+                const uint64_t blk = ((uint64_t)mrow * mw + mcol0 + m) * 6 + slot;
+                uint4 pk;
+                pk.x = (uint32_t)(qv[0] & 0xFFFF) | ((uint32_t)qv[1] << 16);
+                pk.y = (uint32_t)(qv[2] & 0xFFFF) | ((uint32_t)qv[3] << 16);
+                pk.z = (uint32_t)(qv[4] & 0xFFFF) | ((uint32_t)qv[5] << 16);
+                pk.w = (uint32_t)(qv[6] & 0xFFFF) | ((uint32_t)qv[7] << 16);
+                *reinterpret_cast<uint4*>(a.coef + blk * 64 + j * 8) = pk;
+            }
             wave_lds_sync();
         }
-
-        // ---- per-block AC masks and DC values (lane p = zig-zag position) ----
-        const int nblk = nvalid * 6;
-        uint64_t my_mask = 0;
-        int my_dc = 0;
-        for (int b = 0; b < nblk; ++b) {
-            const int v = W.zz[b * 64 + lane];
-            const uint64_t m = __ballot(lane != 0 && v != 0);
-            const int d = __shfl(v, 0);
-            if (lane == b) { my_mask = m; my_dc = d; }
-        }
-
-        // ---- AC symbol histogram (RLE_AC + encode_category, Coding.hpp:148-283) ----
-        if (a.do_hist && lane < nblk) {
-            const int m = lane / 6, k = lane % 6;
-            const int tsel = k < 4 ? 0 : 1;
-            uint64_t ridx;  // block index in the reference's symbol text order (Image.cpp:892-906)
-            if (k < 4) {
-                const uint64_t by = 2ull * mrow + (k >> 1), bx = 2ull * (mcol0 + m) + (k & 1);
-                ridx = by * (2ull * mw) + bx;
-            } else {
-                ridx = (uint64_t)mrow * mw + mcol0 + m + (k == 5 ? (uint64_t)mw * mh : 0ull);
-            }
-            const unsigned long long kb = ridx * 128ull;
-            uint64_t msk = my_mask;
-            int last = 0;
-            while (msk) {
-                const int p = __builtin_ctzll(msk);
-                msk &= msk - 1;
-                const int v = W.zz[lane * 64 + p];
-                const int run = p - last - 1;
-                last = p;
-                const int av = v < 0 ? -v : v;
-                const int cat = 32 - __builtin_clz((unsigned)av);
-                const int sym = ((run & 15) << 4) | cat;
-                atomicAdd(&lds.hcnt[tsel][sym], 1u);
-                atomicMax(&lds.hkey[tsel][sym], ~(kb + 2ull * p + 1ull));
-                if (run >= 16) {
-                    atomicAdd(&lds.hcnt[tsel][0xF0], (unsigned)(run >> 4));
-                    atomicMax(&lds.hkey[tsel][0xF0], ~(kb + 2ull * p));
-                }
-            }
-            if (last < 63) {
-                atomicAdd(&lds.hcnt[tsel][0], 1u);
-                atomicMax(&lds.hkey[tsel][0], ~(kb + 127ull));
-            }
-        }
-
-        // ---- store coefficients / masks / DC (MCU-contiguous) ----
-        const uint64_t mcu0 = (uint64_t)mrow * mw + mcol0;
-        const uint4* zsrc = reinterpret_cast<const uint4*>(W.zz);
-        uint4* zdst = reinterpret_cast<uint4*>(a.coef + mcu0 * 384);
-        const int nchunks = nvalid * 48;  // 768 B per MCU
-        for (int q = lane; q < nchunks; q += 64) zdst[q] = zsrc[q];
-        if (lane < nblk) {
-            a.mask[mcu0 * 6 + lane] = my_mask;
-            a.dc[mcu0 * 6 + lane] = (int16_t)my_dc;
-        }
-        wave_lds_sync();
-    }
-
-    __syncthreads();
-    if (a.do_hist) {
-        const int rep = blockIdx.x % kHistReplicas;
-        for (int i = tid; i < 512; i += kK1Threads) {
-            const int tsel = i >> 8, s = i & 255, gt = tsel ? 3 : 1;
-            const uint32_t c = lds.hcnt[tsel][s];
-            if (c) {
-                atomicAdd(&a.hist.cnt[(rep * 4 + gt) * 256 + s], c);
-                const unsigned long long kk = lds.hkey[tsel][s];
-                unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[gt * 256 + s]);
-                if (kk > *gk) atomicMax(gk, kk);
-            }
-        }
     }
 }
 
-// ---------------------------------------------------------------------------
-// K2 — DC difference statistics
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int category(int v) {
-    const int av = v < 0 ? -v : v;
-    return av ? 32 - __builtin_clz((unsigned)av) : 0;
-}
+// ===========================================================================
+// Shared block staging for K2 / K3: natural-order global blocks -> zig-zag LDS
+// ===========================================================================
+constexpr int kZzStride = 72;  // int16 per staged block (144 B: spreads LDS banks)
 
-__global__ __launch_bounds__(256) void dc_stats_kernel(const int16_t* __restrict__ dc, Geometry g, HistPtrs h) {
-    __shared__ uint32_t hc[2][16];
-    __shared__ unsigned long long hk[2][16];
-    const int tid = threadIdx.x;
-    if (tid < 32) { (&hc[0][0])[tid] = 0; (&hk[0][0])[tid] = 0; }
-    __syncthreads();
-    const uint32_t nmcu = g.nmcu(), mw = g.mw;
-    const uint64_t ncb = nmcu;
-    for (uint32_t m = blockIdx.x * 256 + tid; m < nmcu; m += gridDim.x * 256) {
-        const int16_t* d = dc + (uint64_t)m * 6;
-        const int py = m ? dc[(uint64_t)(m - 1) * 6 + 3] : 0;
-        const int pcb = m ? dc[(uint64_t)(m - 1) * 6 + 4] : 0;
-        const int pcr = m ? dc[(uint64_t)(m - 1) * 6 + 5] : 0;
-        const uint32_t mrow = m / mw, mcol = m % mw;
-        int prev = py;
-        for (int k = 0; k < 4; ++k) {
-            const int c = category(d[k] - prev);
-            prev = d[k];
-            const uint64_t by = 2ull * mrow + (k >> 1), bx = 2ull * mcol + (k & 1);
-            const unsigned long long key = by * 2ull * mw + bx;  // Y-DC text: block raster order
-            atomicAdd(&hc[0][c], 1u);
-            atomicMax(&hk[0][c], ~key);
-        }
-        const int ccb = category(d[4] - pcb), ccr = category(d[5] - pcr);
-        atomicAdd(&hc[1][ccb], 1u);
-        atomicMax(&hk[1][ccb], ~(unsigned long long)m);             // Cb blocks first ...
-        atomicAdd(&hc[1][ccr], 1u);
-        atomicMax(&hk[1][ccr], ~(unsigned long long)(ncb + m));     // ... then Cr blocks
-    }
-    __syncthreads();
-    if (tid < 32) {
-        const int tsel = tid >> 4, s = tid & 15, gt = tsel ? 2 : 0;
-        const uint32_t c = hc[tsel][s];
-        if (c) {
-            const int rep = blockIdx.x % kHistReplicas;
-            atomicAdd(&h.cnt[(rep * 4 + gt) * 256 + s], c);
-            unsigned long long* gk = reinterpret_cast<unsigned long long*>(&h.key[gt * 256 + s]);
-            const unsigned long long kk = hk[tsel][s];
-            if (kk > *gk) atomicMax(gk, kk);
-        }
+template <int kThreads>
+__device__ __forceinline__ void stage_blocks_zz(const int16_t* __restrict__ coef, uint64_t b0, int nb, int16_t* zz,
+                                                int tid) {
+    const uint4* src = reinterpret_cast<const uint4*>(coef + b0 * 64);
+    for (int q = tid; q < nb * 8; q += kThreads) {
+        const uint4 v = src[q];
+        const int blk = q >> 3, row = q & 7;
+        int16_t* d = zz + blk * kZzStride;
+        const uint8_t* z = &kNatToZz[row * 8];
+        d[z[0]] = (int16_t)(v.x & 0xFFFF); d[z[1]] = (int16_t)(v.x >> 16);
+        d[z[2]] = (int16_t)(v.y & 0xFFFF); d[z[3]] = (int16_t)(v.y >> 16);
+        d[z[4]] = (int16_t)(v.z & 0xFFFF); d[z[5]] = (int16_t)(v.z >> 16);
+        d[z[6]] = (int16_t)(v.w & 0xFFFF); d[z[7]] = (int16_t)(v.w >> 16);
     }
 }
 
-// ---------------------------------------------------------------------------
+// Wave-cooperative AC masks: lane p tests zig-zag position p of each block; lane b
+// of wave w ends up holding the mask and DC of block w*64+b.
+__device__ __forceinline__ void block_masks(const int16_t* zz, int wv, int lane, int nb, uint64_t& my_mask,
+                                            int& my_dc) {
+    my_mask = 0;
+    my_dc = 0;
+    const int first = wv * 64;
+    const int cnt = min(64, nb - first);
+    for (int b = 0; b < cnt; ++b) {
+        const int v = zz[(first + b) * kZzStride + lane];
+        const uint64_t m = __ballot(lane != 0 && v != 0);
+        const int d = __builtin_amdgcn_readfirstlane(v);
+        if (lane == b) { my_mask = m; my_dc = d; }
+    }
+}
+
+// DC predecessor of flat block g (Image.cpp:638-678): Y chain runs in MCU order,
+// Cb and Cr each over their own blocks; the first block of each chain predicts 0.
+__device__ __forceinline__ int64_t dc_pred_index(uint64_t g) {
+    const int k = (int)(g % 6);
+    if (k >= 1 && k <= 3) return (int64_t)g - 1;
+    if (g < 6) return -1;
+    return (int64_t)g - (k == 0 ? 3 : 6);
+}
+
+// ===========================================================================
+// K2 — symbol statistics
+// ===========================================================================
+constexpr int kK2Threads = kStatsTile;
+
+struct K2Lds {
+    int16_t zz[kStatsTile * kZzStride];
+    uint32_t cnt[4][256];
+    uint32_t key[4][256];  // workgroup-relative first-occurrence key (min)
+};
+
+__global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
+    __shared__ K2Lds lds;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t nblocks = a.g.nblocks(), mw = a.g.mw;
+    const uint64_t b0 = (uint64_t)blockIdx.x * kStatsTile;
+    const int nb = (int)min((uint64_t)kStatsTile, nblocks - b0);
+    for (int i = tid; i < 1024; i += kK2Threads) {
+        (&lds.cnt[0][0])[i] = 0;
+        (&lds.key[0][0])[i] = 0xFFFFFFFFu;
+    }
+    stage_blocks_zz<kK2Threads>(a.coef, b0, nb, lds.zz, tid);
+    __syncthreads();
+
+    uint64_t msk;
+    int dc;
+    block_masks(lds.zz, wv, lane, nb, msk, dc);
+
+    // key bases: Y raster index of the first Y block row of this tile's first MCU row,
+    // chroma raster index of that MCU row (keys are relative to these inside the tile)
+    const uint32_t mrow0 = (uint32_t)(b0 / 6) / mw;
+    const uint64_t ybase = 2ull * mrow0 * (2ull * mw);
+    const uint64_t cbase = (uint64_t)mrow0 * mw;
+    if (tid < nb) {
+        const uint64_t g = b0 + tid;
+        a.mask[g] = msk;
+        const int64_t pg = dc_pred_index(g);
+        int prev = 0;
+        if (pg >= (int64_t)b0) prev = lds.zz[(pg - b0) * kZzStride];
+        else if (pg >= 0) prev = a.coef[(uint64_t)pg * 64];
+        const int k = (int)(g % 6);
+        const uint64_t m = g / 6;
+        const uint32_t mrow = (uint32_t)(m / mw), mcol = (uint32_t)(m % mw);
+        uint32_t rel;  // position of this block in its symbol text, relative to the tile base
+        int tdc, tac;
+        if (k < 4) {
+            rel = (uint32_t)((2ull * mrow + (k >> 1)) * (2ull * mw) + 2ull * mcol + (k & 1) - ybase);
+            tdc = 0; tac = 1;
+        } else {
+            rel = (uint32_t)(m - cbase) | (k == 5 ? 0x80000000u : 0u);  // all Cr after all Cb
+            tdc = 2; tac = 3;
+        }
+        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
+        const int dcat = category(dc - prev);
+        atomicAdd(&lds.cnt[tdc][dcat], 1u);
+        atomicMin(&lds.key[tdc][dcat], rel);
+        const int16_t* zb = &lds.zz[tid * kZzStride];
+        uint64_t mm = msk;
+        int last = 0;
+        while (mm) {
+            const int p = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int run = p - last - 1;
+            last = p;
+            const int sym = ((run & 15) << 4) | category(zb[p]);
+            atomicAdd(&lds.cnt[tac][sym], 1u);
+            atomicMin(&lds.key[tac][sym], acb + 2u * p + 1u);
+            if (run >= 16) {
+                atomicAdd(&lds.cnt[tac][0xF0], (uint32_t)(run >> 4));
+                atomicMin(&lds.key[tac][0xF0], acb + 2u * p);
+            }
+        }
+        if (last < 63) {  // EOB
+            atomicAdd(&lds.cnt[tac][0], 1u);
+            atomicMin(&lds.key[tac][0], acb + 127u);
+        }
+    }
+    __syncthreads();
+
+    const int rep = blockIdx.x % kHistReplicas;
+    const uint64_t ncb = a.g.nmcu();
+    for (int i = tid; i < 1024; i += kK2Threads) {
+        const int t = i >> 8, s = i & 255;
+        const uint32_t c = lds.cnt[t][s];
+        if (!c) continue;
+        atomicAdd(&a.hist.cnt[(rep * 4 + t) * 256 + s], c);
+        const uint32_t k32 = lds.key[t][s];
+        const bool ac = t & 1;
+        uint64_t base;
+        if (t < 2) base = ybase;
+        else base = (k32 & 0x80000000u) ? ncb + cbase : cbase;
+        const uint64_t gkey = (ac ? base * 128ull : base) + (k32 & 0x7FFFFFFFu);
+        const unsigned long long inv = ~gkey;
+        unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[t * 256 + s]);
+        if (inv > *gk) atomicMax(gk, inv);
+    }
+}
+
+// ===========================================================================
 // K3 — entropy coding with two decoupled look-back scans
-// ---------------------------------------------------------------------------
+// ===========================================================================
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr uint32_t kSpinLimit = 1u << 22;
 
 __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -378,48 +390,65 @@ __device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Single-lane decoupled look-back; records are self-contained 8-byte granules
-// {flag, value} written by one store, so no payload fence is needed.
-__device__ uint64_t lookback(uint64_t* rec, uint32_t tile, uint64_t agg, uint64_t* err) {
-    if (tile == 0) { st_relaxed(&rec[0], kFlagIncl | agg); return 0; }
-    st_relaxed(&rec[tile], kFlagAgg | agg);
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// Decoupled look-back run by one whole wave: each pass inspects 64 predecessors.
+// Records are self-contained 8-byte {flag, value} granules (one relaxed agent-scope
+// store each), so no payload fence is needed.  Returns the exclusive prefix.
+__device__ uint64_t lookback_wave(uint64_t* rec, uint32_t tile, uint64_t agg, uint64_t* err, int lane) {
+    if (tile == 0) {
+        if (lane == 0) st_relaxed(&rec[0], kFlagIncl | agg);
+        return 0;
+    }
+    if (lane == 0) st_relaxed(&rec[tile], kFlagAgg | agg);
     uint64_t excl = 0;
-    int64_t j = (int64_t)tile - 1;
+    int64_t end = tile;
     uint32_t spins = 0;
-    while (j >= 0) {
-        const uint64_t r = ld_relaxed(&rec[j]);
+    for (;;) {
+        const int64_t idx = end - 1 - lane;
+        const uint64_t r = idx >= 0 ? ld_relaxed(&rec[idx]) : kFlagIncl;
         const uint64_t f = r & ~kValMask;
-        if (f == 0) {
-            if (++spins > kSpinLimit) { atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull); break; }
-            __builtin_amdgcn_s_sleep(1);
+        const uint64_t incl = __ballot(f == kFlagIncl);
+        const uint64_t notready = __ballot(f == 0);
+        const int first = incl ? __builtin_ctzll(incl) : 64;
+        const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+        if (notready & upto) {
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        excl += r & kValMask;
-        if (f == kFlagIncl) break;
-        --j;
+        excl += wave_sum64(lane <= first ? (r & kValMask) : 0ull);
+        if (first < 64) break;
+        end -= 64;
     }
-    st_relaxed(&rec[tile], kFlagIncl | (excl + agg));
+    if (lane == 0) st_relaxed(&rec[tile], kFlagIncl | (excl + agg));
     return excl;
 }
 
-// MSB-first bit sink over big-endian 32-bit LDS words; the first word of a
-// thread's run may be shared with the previous thread, so words are OR-ed.
+// MSB-first bit sink over big-endian 32-bit LDS words; a thread's first and last
+// words may be shared with its neighbours, so every word is OR-ed in.
 struct BitSink {
     uint32_t* st;
     uint32_t word;
-    int fill;       // bits already placed in the current word (leading bits are others')
-    uint64_t acc;   // right-aligned pending bits of the current word
-    __device__ __forceinline__ void init(uint32_t* s, uint64_t pos) {
-        st = s; word = (uint32_t)(pos >> 5); fill = (int)(pos & 31); acc = 0;
+    int fill;      // bits placed in the current word (leading bits belong to others)
+    uint64_t acc;  // right-aligned pending bits of the current word
+    __device__ __forceinline__ void init(uint32_t* s, uint32_t pos) {
+        st = s; word = pos >> 5; fill = (int)(pos & 31); acc = 0;
     }
     __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
-        if (n == 0) return;
         acc = (acc << n) | v;
         fill += n;
         if (fill >= 32) {
             fill -= 32;
             atomicOr(&st[word++], (uint32_t)(acc >> fill));
-            acc &= (fill ? ((1ull << fill) - 1) : 0ull);
+            acc &= (1ull << fill) - 1;
         }
     }
     __device__ __forceinline__ void flush() {
@@ -433,9 +462,10 @@ __device__ __forceinline__ uint32_t stage_byte(const uint32_t* st, uint32_t i) {
 
 constexpr int kK3Threads = kEntropyTile;
 constexpr int kStageWords = kEntropyTile * kStageBytesPerBlock / 4 + 2;
+constexpr int kOutLdsBytes = kEntropyTile * kZzStride * 2;
 
 __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
-    __shared__ int16_t coef[kEntropyTile * 64];
+    __shared__ int16_t zz[kEntropyTile * kZzStride];  // reused as the stuffed-output buffer
     __shared__ uint32_t stage[kStageWords];
     __shared__ uint32_t tab[4 * 256];
     __shared__ uint32_t wsum[kK3Threads / 64];
@@ -452,47 +482,40 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
     const bool last_tile = tile == ntiles - 1;
     const uint64_t b0 = (uint64_t)tile * kEntropyTile;
     const int nb = (int)min((uint64_t)kEntropyTile, nblocks - b0);
+    stage_blocks_zz<kK3Threads>(a.coef, b0, nb, zz, tid);
+    __syncthreads();
 
-    // coefficients of the tile: contiguous [nb][64] int16 (16-byte chunks)
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.coef + b0 * 64);
-        uint4* dst = reinterpret_cast<uint4*>(coef);
-        for (int q = tid; q < nb * 8; q += kK3Threads) dst[q] = src[q];
-    }
     const bool active = tid < nb;
     const uint64_t g = b0 + tid;
     const int k = (int)(g % 6);
-    const uint64_t m = g / 6;
     uint64_t msk = 0;
     int dcdiff = 0;
+    const int16_t* zb = &zz[tid * kZzStride];
     if (active) {
         msk = a.mask[g];
-        // DC predecessor (Image.cpp:638-678): Y chain in MCU order, Cb/Cr per component.
-        const int cur = a.dc[g];
+        const int64_t pg = dc_pred_index(g);
         int prev = 0;
-        if (k >= 1 && k <= 3) prev = a.dc[g - 1];
-        else if (m > 0) prev = a.dc[g - (k == 0 ? 3 : 6)];
-        dcdiff = cur - prev;
+        if (pg >= (int64_t)b0) prev = zz[(pg - b0) * kZzStride];
+        else if (pg >= 0) prev = a.coef[(uint64_t)pg * 64];
+        dcdiff = zb[0] - prev;
     }
     const uint32_t* tdc = &tab[(k < 4 ? 0 : 2) * 256];
     const uint32_t* tac = &tab[(k < 4 ? 1 : 3) * 256];
-    __syncthreads();
 
     // ---- pass 1: bit length of this block ----
     uint32_t nbits = 0;
-    const int16_t* cb = &coef[tid * 64];
     if (active) {
         const int dcat = category(dcdiff);
         nbits = (tdc[dcat] >> 16) + dcat;
+        const uint32_t zrl = tac[0xF0] >> 16;
         uint64_t mm = msk;
         int last = 0;
-        const uint32_t zrl = tac[0xF0] >> 16;
         while (mm) {
             const int p = __builtin_ctzll(mm);
             mm &= mm - 1;
             const int run = p - last - 1;
             last = p;
-            const int cat = category(cb[p]);
+            const int cat = category(zb[p]);
             nbits += (uint32_t)(run >> 4) * zrl + (tac[((run & 15) << 4) | cat] >> 16) + cat;
         }
         if (last < 63) nbits += tac[0] >> 16;
@@ -508,14 +531,18 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
     uint32_t wbase = 0, total = 0;
+#pragma unroll
     for (int w = 0; w < kK3Threads / 64; ++w) {
         if (w < wv) wbase += wsum[w];
         total += wsum[w];
     }
     const uint32_t excl_bits = wbase + incl - nbits;
 
-    // ---- look-back 1: global bit offset ----
-    if (tid == 0) s_prefix = lookback(a.lb_bits, tile, total, a.result + 1);
+    // ---- look-back 1: global bit offset of this tile ----
+    if (wv == 0) {
+        const uint64_t pre = lookback_wave(a.lb_bits, tile, total, a.result + 1, lane);
+        if (lane == 0) s_prefix = pre;
+    }
     __syncthreads();
     const uint64_t P = s_prefix;
     const uint32_t lead = (uint32_t)(P & 7);
@@ -530,31 +557,29 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
         bs.init(stage, lead + excl_bits);
         const int dcat = category(dcdiff);
         const uint32_t dce = tdc[dcat];
-        const uint32_t dbits = dcdiff < 0 ? (uint32_t)(dcdiff + (1 << dcat) - 1) : (uint32_t)dcdiff;
-        bs.put(dce & 0xFFFF, (int)(dce >> 16));
-        bs.put(dcat ? (dbits & ((1u << dcat) - 1)) : 0u, dcat);
+        const uint32_t dbits = (uint32_t)(dcdiff < 0 ? dcdiff + (1 << dcat) - 1 : dcdiff) & ((1u << dcat) - 1);
+        bs.put(((dce & 0xFFFF) << dcat) | dbits, (int)(dce >> 16) + dcat);
+        const uint32_t zrl = tac[0xF0];
         uint64_t mm = msk;
         int last = 0;
-        const uint32_t zrl = tac[0xF0];
         while (mm) {
             const int p = __builtin_ctzll(mm);
             mm &= mm - 1;
             int run = p - last - 1;
             last = p;
             while (run >= 16) { bs.put(zrl & 0xFFFF, (int)(zrl >> 16)); run -= 16; }
-            const int v = cb[p];
+            const int v = zb[p];
             const int cat = category(v);
             const uint32_t e = tac[(run << 4) | cat];
-            const uint32_t vb = v < 0 ? (uint32_t)(v + (1 << cat) - 1) : (uint32_t)v;
-            bs.put(e & 0xFFFF, (int)(e >> 16));
-            bs.put(vb & ((1u << cat) - 1), cat);
+            const uint32_t vb = (uint32_t)(v < 0 ? v + (1 << cat) - 1 : v) & ((1u << cat) - 1);
+            bs.put(((e & 0xFFFF) << cat) | vb, (int)(e >> 16) + cat);
         }
         if (last < 63) { const uint32_t e = tac[0]; bs.put(e & 0xFFFF, (int)(e >> 16)); }
         bs.flush();
     }
     __syncthreads();
 
-    // ---- boundary byte: publish own tail, merge predecessor's tail; 1-fill at the end ----
+    // ---- boundary byte: publish own tail, merge the predecessor's; 1-fill at the end ----
     if (tid == 0) {
         if (!last_tile) {
             const uint32_t tb = (endbit & 7) ? stage_byte(stage, endbit >> 3) : 0u;
@@ -567,15 +592,18 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
         if (lead && tile > 0) {
             uint32_t t = 0, spins = 0;
             while (!((t = __hip_atomic_load(&a.tails[tile - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 31)) {
-                if (++spins > kSpinLimit) { atomicOr(reinterpret_cast<unsigned long long*>(a.result + 1), 2ull); break; }
-                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit) {
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.result + 1), 2ull);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
             }
             stage[0] |= (t & 0xFF) << 24;
         }
     }
     __syncthreads();
 
-    // ---- 0xFF count over the bytes this tile owns ----
+    // ---- 0xFF count over the bytes this tile owns (byte owner = tile of its last bit) ----
     const uint32_t nown = (endbit >> 3) + ((last_tile && (endbit & 7)) ? 1u : 0u);
     const uint32_t per = (nown + kK3Threads - 1) / kK3Threads;
     const uint32_t lo = min(nown, (uint32_t)tid * per), hi = min(nown, lo + per);
@@ -587,10 +615,10 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
         const uint32_t o = __shfl_up(fincl, d);
         if (lane >= d) fincl += o;
     }
-    __syncthreads();
     if (lane == 63) wsum[wv] = fincl;
     __syncthreads();
     uint32_t fbase = 0, ftotal = 0;
+#pragma unroll
     for (int w = 0; w < kK3Threads / 64; ++w) {
         if (w < wv) fbase += wsum[w];
         ftotal += wsum[w];
@@ -598,35 +626,63 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
     const uint32_t ff_before = fbase + fincl - nff;
 
     // ---- look-back 2: stuffed-byte offset ----
-    if (tid == 0) s_ffprefix = lookback(a.lb_ff, tile, ftotal, a.result + 1);
+    if (wv == 0) {
+        const uint64_t pre = lookback_wave(a.lb_ff, tile, ftotal, a.result + 1, lane);
+        if (lane == 0) s_ffprefix = pre;
+    }
     __syncthreads();
-    const uint64_t Q = s_ffprefix;
-    const uint64_t base = a.hdr_len + (P >> 3) + Q;
-    const uint64_t end_total = base + nown + ftotal + (last_tile ? 2 : 0);
-    if (end_total > a.out_cap) {
+    const uint64_t D0 = a.hdr_len + (P >> 3) + s_ffprefix;  // first output byte of this tile
+    const uint32_t ntot = nown + ftotal + (last_tile ? 2u : 0u);
+    if (D0 + ntot > a.out_cap) {
         if (tid == 0) atomicOr(reinterpret_cast<unsigned long long*>(a.result + 1), 4ull);
         return;
     }
-    uint64_t o = base + lo + ff_before;
-    for (uint32_t i = lo; i < hi; ++i) {
-        const uint8_t b = (uint8_t)stage_byte(stage, i);
-        a.out[o++] = b;
-        if (b == 0xFF) a.out[o++] = 0;
+    const uint32_t align = (uint32_t)(D0 & 3);
+    if (align + ntot <= (uint32_t)kOutLdsBytes) {
+        // stuff into LDS (reusing the coefficient buffer), then aligned 4-byte stores
+        uint8_t* ob = reinterpret_cast<uint8_t*>(zz);
+        uint32_t o = align + lo + ff_before;
+        for (uint32_t i = lo; i < hi; ++i) {
+            const uint8_t b = (uint8_t)stage_byte(stage, i);
+            ob[o++] = b;
+            if (b == 0xFF) ob[o++] = 0;
+        }
+        if (last_tile && tid == 0) {
+            ob[align + nown + ftotal] = 0xFF;
+            ob[align + nown + ftotal + 1] = 0xD9;
+        }
+        __syncthreads();
+        uint8_t* gout = a.out + (D0 - align);
+        const uint32_t nw = (align + ntot + 3) / 4;
+        for (uint32_t w = tid; w < nw; w += kK3Threads) {
+            const uint32_t s = 4 * w, e = s + 4;
+            if (s >= align && e <= align + ntot) {
+                *reinterpret_cast<uint32_t*>(gout + s) = *reinterpret_cast<const uint32_t*>(ob + s);
+            } else {
+                for (uint32_t q = max(s, align); q < min(e, align + ntot); ++q) gout[q] = ob[q];
+            }
+        }
+    } else {
+        uint64_t o = D0 + lo + ff_before;
+        for (uint32_t i = lo; i < hi; ++i) {
+            const uint8_t b = (uint8_t)stage_byte(stage, i);
+            a.out[o++] = b;
+            if (b == 0xFF) a.out[o++] = 0;
+        }
+        if (last_tile && tid == 0) {
+            a.out[D0 + nown + ftotal] = 0xFF;
+            a.out[D0 + nown + ftotal + 1] = 0xD9;
+        }
     }
-    if (last_tile && tid == 0) {
-        const uint64_t e = base + nown + ftotal;
-        a.out[e] = 0xFF;
-        a.out[e + 1] = 0xD9;
-        a.result[0] = e + 2;
-    }
+    if (last_tile && tid == 0) a.result[0] = D0 + ntot;
 }
 
 }  // namespace
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
     const uint32_t tiles = ((a.g.mw + 3) / 4) * a.g.mh;
-    const uint32_t wgs_needed = (tiles + 3) / 4;
-    const uint32_t grid = wgs_needed < 1024 ? wgs_needed : 1024;
+    const uint32_t wgs = (tiles + 3) / 4;
+    const uint32_t grid = wgs < 2048 ? wgs : 2048;
     if (a.maxval == 255)
         hipLaunchKernelGGL(fdct_kernel<true>, dim3(grid), dim3(kK1Threads), 0, s, a);
     else
@@ -634,10 +690,9 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_dc_stats(const int16_t* dc, const Geometry& g, HistPtrs h, hipStream_t s) {
-    uint32_t grid = (g.nmcu() + 255) / 256;
-    if (grid > 512) grid = 512;
-    hipLaunchKernelGGL(dc_stats_kernel, dim3(grid), dim3(256), 0, s, dc, g, h);
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
+    const uint32_t grid = (a.g.nblocks() + kStatsTile - 1) / kStatsTile;
+    hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(kK2Threads), 0, s, a);
     return hipGetLastError();
 }
 

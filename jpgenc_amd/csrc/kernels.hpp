@@ -1,5 +1,12 @@
 // Device-side interface of the jpge HIP kernels (gfx950).  Host code fills
 // these parameter blocks; kernels.hip owns the launch geometry.
+//
+// Data layout in HBM (per frame):
+//   rgb   : interleaved RGB8, row pitch `stride` (16-byte aligned pitch/base = fast path)
+//   coef  : int16 [nmcu][6][64]  quantised coefficients, NATURAL order inside a block,
+//           blocks in MCU-interleave order Y00 Y01 Y10 Y11 Cb Cr (= entropy order)
+//   mask  : u64   [nmcu][6]      AC non-zero mask, bit p = zig-zag position p (1..63)
+//   hist  : u32 cnt[kHistReplicas][4][256], u64 key[4][256] (~first-occurrence key)
 #pragma once
 #include <cstdint>
 
@@ -22,35 +29,36 @@ struct Geometry {
     JPGE_HD uint32_t nblocks() const { return nmcu() * 6; }
 };
 
-constexpr int kHistReplicas = 8;        // spread of the global histogram atomics
-constexpr int kEntropyTile = 128;       // blocks per entropy workgroup
+constexpr int kHistReplicas = 8;          // spread of the global histogram atomics
+constexpr int kStatsTile = 256;           // blocks per statistics workgroup
+constexpr int kEntropyTile = 128;         // blocks per entropy workgroup
 constexpr int kStageBytesPerBlock = 216;  // >= worst-case 1665 bits of one block
 
-// Histogram layout (device): cnt[kHistReplicas][4][256] u32, key[4][256] u64
-// holding ~first_key (so atomicMax keeps the minimum key).  Tables: 0 Y-DC,
-// 1 Y-AC, 2 C-DC, 3 C-AC.
+// Tables: 0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC.
 struct HistPtrs {
     uint32_t* cnt;
     uint64_t* key;
 };
 
 struct FdctArgs {
-    const uint8_t* rgb;     // device, interleaved RGB8, row pitch `stride` bytes
+    const uint8_t* rgb;
     uint64_t stride;
     Geometry g;
-    int maxval;             // 255 -> exact integer colour path
-    const double* qtab;     // device [128]: luma then chroma, natural order
-    int16_t* coef;          // [nmcu][6][64] zig-zag order
-    uint64_t* mask;         // [nmcu][6] AC non-zero masks (bit p = zig-zag position p)
-    int16_t* dc;            // [nmcu][6] quantised DC
-    HistPtrs hist;          // AC tables filled here (when do_hist)
-    int do_hist;
+    int maxval;          // 255 -> exact integer colour path
+    const double* qtab;  // [128]: luma then chroma, natural order
+    int16_t* coef;
+};
+
+struct StatsArgs {
+    const int16_t* coef;
+    uint64_t* mask;
+    Geometry g;
+    HistPtrs hist;
 };
 
 struct EntropyArgs {
     const int16_t* coef;
     const uint64_t* mask;
-    const int16_t* dc;
     Geometry g;
     const uint32_t* tables;  // [4][256] (len << 16) | code
     uint8_t* out;            // whole .jpg (header already at [0, hdr_len))
@@ -63,13 +71,12 @@ struct EntropyArgs {
     uint64_t* result;        // [0] total .jpg bytes, [1] error bits
 };
 
-// Workspace sizing helpers.
 inline uint32_t entropy_tiles(const Geometry& g) {
     return (g.nblocks() + kEntropyTile - 1) / kEntropyTile;
 }
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s);
-hipError_t launch_dc_stats(const int16_t* dc, const Geometry& g, HistPtrs h, hipStream_t s);
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s);
 
 }  // namespace jpge
