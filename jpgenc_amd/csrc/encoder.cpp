@@ -1,6 +1,7 @@
 #include "encoder.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace jpge {
@@ -56,6 +57,8 @@ struct Encoder::Slot {
     int16_t* d_coef = nullptr;
     uint64_t* d_mask = nullptr;
     uint8_t* d_ctl = nullptr;
+    uint32_t* d_scratch = nullptr;
+    size_t cap_scratch = 0;
     uint8_t* d_out = nullptr;
     double* d_q = nullptr;
     uint32_t* d_tab = nullptr;
@@ -76,7 +79,7 @@ struct Encoder::Slot {
     uint8_t qy[64], qc[64];
 
     ~Slot() {
-        hipFree(d_in); hipFree(d_coef); hipFree(d_mask); hipFree(d_ctl);
+        hipFree(d_in); hipFree(d_coef); hipFree(d_mask); hipFree(d_ctl); hipFree(d_scratch);
         hipFree(d_out); hipFree(d_q); hipFree(d_tab);
         hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_hdr); hipHostFree(h_result); hipHostFree(h_q);
         for (auto& e : ev) if (e) hipEventDestroy(e);
@@ -98,6 +101,8 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     JPGE_HIP(hipSetDevice(device));
     std::unique_ptr<Encoder> e(new Encoder());
     e->device_ = device;
+    const char* fg = std::getenv("JPGE_FORCE_GLOBAL_STAGE");
+    e->force_global_stage_ = fg && fg[0] == '1';
     for (int i = 0; i < 3; ++i) {
         std::unique_ptr<Slot> s(new Slot());
         JPGE_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
@@ -131,6 +136,12 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         s.cap_mcu = nmcu;
     }
     const CtlLayout L(entropy_tiles(g));
+    const size_t scratch = (size_t)entropy_tiles(g) * kScratchWordsPerTile * 4;
+    if (scratch > s.cap_scratch) {
+        hipFree(s.d_scratch); s.d_scratch = nullptr; s.cap_scratch = 0;
+        JPGE_HIP(hipMalloc((void**)&s.d_scratch, scratch));
+        s.cap_scratch = scratch;
+    }
     if (L.total > s.cap_ctl) {
         hipFree(s.d_ctl); s.d_ctl = nullptr; s.cap_ctl = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_ctl, L.total));
@@ -267,6 +278,8 @@ int Encoder::phase2(Slot& s, const FrameDesc& f, uint32_t flags) {
     e.lb_ff = reinterpret_cast<uint64_t*>(s.d_ctl + L.lb_ff);
     e.tails = reinterpret_cast<uint32_t*>(s.d_ctl + L.tails);
     e.result = reinterpret_cast<uint64_t*>(s.d_ctl + L.result);
+    e.scratch = s.d_scratch;
+    e.stage_cap = force_global_stage_ ? 0u : 0xFFFFFFFFu;
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
     JPGE_HIP(launch_entropy(e, s.stream));
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[5], s.stream));

@@ -69,6 +69,7 @@ class Encoder {
 
     int device_ = 0;
     bool timing_ = false;
+    bool force_global_stage_ = false;  // JPGE_FORCE_GLOBAL_STAGE=1: exercise the K3 fallback (tests)
     KernelTimes times_;
     std::vector<std::unique_ptr<Slot>> slots_;
 };

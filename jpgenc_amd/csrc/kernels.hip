@@ -74,8 +74,20 @@ __device__ __forceinline__ void arai8(const double x[8], double o[8]) {
 }
 
 // quantize, Coding.hpp:92-94: (int)std::round(d / q) — correctly rounded fp64
-// division, then round half away from zero.
-__device__ __forceinline__ int quant1(double d, double q) { return (int)round(d / q); }
+// division, then round half away from zero.  Fast path: r = d * (1/q) is within
+// ~2 ulp of the true quotient, so round(r) == round(fl(d/q)) unless r lies within
+// 2^-30 of a half-integer (|q| >= 1, |d/q| < 2^20 keep that bound far above the
+// error); those rare cases take the exact division.  Integer boundaries are
+// harmless: a quotient on either side of k rounds to k either way.
+__device__ __forceinline__ int quant1(double d, double q, double invq) {
+    const double r = d * invq;
+    const double a = __builtin_fabs(r);
+    const double fl = __builtin_floor(a);
+    const double f = a - fl;
+    if (__builtin_fabs(f - 0.5) < 0x1p-30 || a >= 0x1p20) return (int)round(d / q);
+    const int n = (int)fl + (f > 0.5 ? 1 : 0);
+    return r < 0 ? -n : n;
+}
 
 // ===========================================================================
 // K1 — colour + 4:2:0 + FDCT + quantise
@@ -89,9 +101,11 @@ struct K1WaveLds {
     uint32_t rgbx[16 * kRgbPitch];  // packed R | G<<8 | B<<16
     double tmp[8 * kTmpBlock];      // pass-1 output, transposed
 };
+constexpr int kQRow = 9;  // padded q-table rows: lanes reading rows j=0..7 hit distinct banks
 struct K1Lds {
     K1WaveLds w[4];
-    double q[128];
+    double q[2][8 * kQRow];     // luma, chroma
+    double invq[2][8 * kQRow];  // 1/q (correctly rounded)
 };
 
 __device__ __forceinline__ double ycc_exact_y(uint32_t p) {
@@ -117,7 +131,11 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
     __shared__ K1Lds lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     K1WaveLds& W = lds.w[wv];
-    for (int i = tid; i < 128; i += kK1Threads) lds.q[i] = a.qtab[i];
+    for (int i = tid; i < 128; i += kK1Threads) {
+        const int c = i >> 6, e = i & 63, o = (e >> 3) * kQRow + (e & 7);
+        lds.q[c][o] = a.qtab[i];
+        lds.invq[c][o] = 1.0 / a.qtab[i];
+    }
     __syncthreads();
 
     const uint32_t mw = a.g.mw;
@@ -129,17 +147,32 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
     const int r16 = lane >> 2, c16 = lane & 3;  // staging: lane -> (pixel row, 16-px chunk)
     const int b8 = lane >> 3, j = lane & 7;     // DCT: lane -> (block of the round, column)
 
-    for (uint32_t t = blockIdx.x * 4 + wv; t < ntiles; t += nwaves) {
+    // 48-byte RGB run of this lane for tile t, if the tile is on the aligned fast path
+    auto fast_load = [&](uint32_t t, uint4& v0, uint4& v1, uint4& v2) -> bool {
+        const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * 4;
+        const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
+        if (!(aligned && y < a.g.height && xs + 16 <= a.g.width)) return false;
+        const uint4* src = reinterpret_cast<const uint4*>(a.rgb + (uint64_t)y * a.stride + (uint64_t)xs * 3);
+        v0 = src[0]; v1 = src[1]; v2 = src[2];
+        return true;
+    };
+    uint32_t t = blockIdx.x * 4 + wv;
+    uint4 c0 = {}, c1 = {}, c2 = {};
+    bool cfast = t < ntiles && fast_load(t, c0, c1, c2);
+
+    for (; t < ntiles; t += nwaves) {
         const uint32_t mrow = t / tiles_per_row;
         const uint32_t mcol0 = (t % tiles_per_row) * 4;
         const int nvalid = (int)min(4u, mw - mcol0);
         const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
+        // prefetch the next tile of this wave while this one is transformed
+        uint4 n0 = {}, n1 = {}, n2 = {};
+        const bool nfast = t + nwaves < ntiles && fast_load(t + nwaves, n0, n1, n2);
 
         // ---- stage 16 px per lane as packed u32 ----
         uint32_t px[16];
-        if (aligned && y < a.g.height && xs + 16 <= a.g.width) {
-            const uint4* src = reinterpret_cast<const uint4*>(a.rgb + (uint64_t)y * a.stride + (uint64_t)xs * 3);
-            const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+        if (cfast) {
+            const uint4 v0 = c0, v1 = c1, v2 = c2;
             const uint32_t wd[13] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, 0u};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -204,7 +237,7 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
                     }
                 }
                 slot = 4 + comp;
-                qb = 64;
+                qb = 1;
             }
             // column pass, written transposed (Dct.hpp:124-131); row pass
             double o[8];
@@ -218,7 +251,8 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
             arai8(x, o);  // o[u] = y(j, u)
             int qv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) qv[u] = quant1(o[u], lds.q[qb + j * 8 + u]);
+            for (int u = 0; u < 8; ++u)
+                qv[u] = quant1(o[u], lds.q[qb][j * kQRow + u], lds.invq[qb][j * kQRow + u]);
             if (m < nvalid) {
                 const uint64_t blk = ((uint64_t)mrow * mw + mcol0 + m) * 6 + slot;
                 uint4 pk;
@@ -230,14 +264,19 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
             }
             wave_lds_sync();
         }
+        c0 = n0; c1 = n1; c2 = n2;
+        cfast = nfast;
     }
 }
 
-// ===========================================================================
-// Shared block staging for K2 / K3: natural-order global blocks -> zig-zag LDS
-// ===========================================================================
-constexpr int kZzStride = 72;  // int16 per staged block (144 B: spreads LDS banks)
 
+// ===========================================================================
+// Shared pieces of K2 / K3
+// ===========================================================================
+constexpr int kZzStride = 72;    // int16 per staged block (144 B: spreads LDS banks)
+constexpr int kPartsPerBlock = 4;  // lanes cooperating on one block's non-zero coefficients
+
+// natural-order global blocks -> zig-zag-ordered LDS blocks
 template <int kThreads>
 __device__ __forceinline__ void stage_blocks_zz(const int16_t* __restrict__ coef, uint64_t b0, int nb, int16_t* zz,
                                                 int tid) {
@@ -254,24 +293,8 @@ __device__ __forceinline__ void stage_blocks_zz(const int16_t* __restrict__ coef
     }
 }
 
-// Wave-cooperative AC masks: lane p tests zig-zag position p of each block; lane b
-// of wave w ends up holding the mask and DC of block w*64+b.
-__device__ __forceinline__ void block_masks(const int16_t* zz, int wv, int lane, int nb, uint64_t& my_mask,
-                                            int& my_dc) {
-    my_mask = 0;
-    my_dc = 0;
-    const int first = wv * 64;
-    const int cnt = min(64, nb - first);
-    for (int b = 0; b < cnt; ++b) {
-        const int v = zz[(first + b) * kZzStride + lane];
-        const uint64_t m = __ballot(lane != 0 && v != 0);
-        const int d = __builtin_amdgcn_readfirstlane(v);
-        if (lane == b) { my_mask = m; my_dc = d; }
-    }
-}
-
-// DC predecessor of flat block g (Image.cpp:638-678): Y chain runs in MCU order,
-// Cb and Cr each over their own blocks; the first block of each chain predicts 0.
+// DC predecessor of flat block g (Image.cpp:638-678): the Y chain runs in MCU
+// order, Cb and Cr each over their own blocks; a chain's first block predicts 0.
 __device__ __forceinline__ int64_t dc_pred_index(uint64_t g) {
     const int k = (int)(g % 6);
     if (k >= 1 && k <= 3) return (int64_t)g - 1;
@@ -279,81 +302,138 @@ __device__ __forceinline__ int64_t dc_pred_index(uint64_t g) {
     return (int64_t)g - (k == 0 ? 3 : 6);
 }
 
+// position of the k-th (0-based) set bit of m (k < popcount(m))
+__device__ __forceinline__ int kth_set_bit(uint64_t m, int k) {
+    uint32_t w = (uint32_t)m;
+    int pos = 0, c = __builtin_popcount(w);
+    if (k >= c) { k -= c; w = (uint32_t)(m >> 32); pos = 32; }
+    c = __builtin_popcount(w & 0xFFFFu);
+    if (k >= c) { k -= c; w >>= 16; pos += 16; }
+    c = __builtin_popcount(w & 0xFFu);
+    if (k >= c) { k -= c; w >>= 8; pos += 8; }
+    c = __builtin_popcount(w & 0xFu);
+    if (k >= c) { k -= c; w >>= 4; pos += 4; }
+    for (; k > 0; --k) w &= w - 1;
+    return pos + __builtin_ctz(w);
+}
+
+// One lane's share of a block's AC symbols: the non-zero coefficients with rank
+// [lo, hi) in zig-zag order.  `last` is the zig-zag position of the non-zero just
+// before the first one of this share (0 = the DC position), `m` the mask of the
+// positions still to visit, `cnt` how many of them belong to this share.
+struct Share {
+    uint64_t m;
+    int last, cnt;
+    __device__ __forceinline__ void init(uint64_t mask, int part) {
+        const int n = __builtin_popcountll(mask);
+        const int per = (n + kPartsPerBlock - 1) / kPartsPerBlock;
+        const int lo = min(n, part * per), hi = min(n, lo + per);
+        cnt = hi - lo;
+        if (lo == 0) {
+            m = mask;
+            last = 0;
+        } else {
+            last = kth_set_bit(mask, lo - 1);
+            m = last >= 63 ? 0ull : mask & ~((2ull << last) - 1);
+        }
+    }
+};
+
 // ===========================================================================
-// K2 — symbol statistics
+// K2 — symbol statistics (4 lanes per block)
 // ===========================================================================
-constexpr int kK2Threads = kStatsTile;
+constexpr int kK2Blocks = kStatsTile;
+constexpr int kK2Threads = kK2Blocks * kPartsPerBlock;
+constexpr int kHistCopies = 8;  // LDS copies of the AC counters: caps same-address atomics at 8 lanes
 
 struct K2Lds {
-    int16_t zz[kStatsTile * kZzStride];
-    uint32_t cnt[4][256];
-    uint32_t key[4][256];  // workgroup-relative first-occurrence key (min)
+    int16_t zz[kK2Blocks * kZzStride];
+    uint32_t acnt[kHistCopies][2][256];  // AC counters (Y-AC, C-AC), per copy
+    uint32_t dcnt[2][16];                // DC counters (Y-DC, C-DC)
+    uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
+    uint64_t bmask[kK2Blocks];
 };
 
 __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     __shared__ K2Lds lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t nblocks = a.g.nblocks(), mw = a.g.mw;
-    const uint64_t b0 = (uint64_t)blockIdx.x * kStatsTile;
-    const int nb = (int)min((uint64_t)kStatsTile, nblocks - b0);
-    for (int i = tid; i < 1024; i += kK2Threads) {
-        (&lds.cnt[0][0])[i] = 0;
-        (&lds.key[0][0])[i] = 0xFFFFFFFFu;
-    }
+    const uint64_t b0 = (uint64_t)blockIdx.x * kK2Blocks;
+    const int nb = (int)min((uint64_t)kK2Blocks, nblocks - b0);
+    for (int i = tid; i < kHistCopies * 512; i += kK2Threads) (&lds.acnt[0][0][0])[i] = 0;
+    for (int i = tid; i < 1024; i += kK2Threads) (&lds.key[0][0])[i] = 0xFFFFFFFFu;
+    if (tid < 32) (&lds.dcnt[0][0])[tid] = 0;
     stage_blocks_zz<kK2Threads>(a.coef, b0, nb, lds.zz, tid);
     __syncthreads();
 
-    uint64_t msk;
-    int dc;
-    block_masks(lds.zz, wv, lane, nb, msk, dc);
+    // AC masks: lane p tests zig-zag position p; each wave covers 16 blocks
+    constexpr int kPerWave = kK2Blocks / (kK2Threads / 64);
+    for (int i = 0; i < kPerWave; ++i) {
+        const int blk = wv * kPerWave + i;
+        if (blk >= nb) break;
+        const int v = lds.zz[blk * kZzStride + lane];
+        const uint64_t m = __ballot(lane != 0 && v != 0);
+        if (lane == 0) {
+            lds.bmask[blk] = m;
+            a.mask[b0 + blk] = m;
+        }
+    }
+    __syncthreads();
 
-    // key bases: Y raster index of the first Y block row of this tile's first MCU row,
-    // chroma raster index of that MCU row (keys are relative to these inside the tile)
+    const int blk = tid / kPartsPerBlock, part = tid % kPartsPerBlock;
+    // key bases: Y raster index of the first Y block row of this tile's first MCU
+    // row, chroma raster index of that MCU row (keys are relative inside the tile)
     const uint32_t mrow0 = (uint32_t)(b0 / 6) / mw;
     const uint64_t ybase = 2ull * mrow0 * (2ull * mw);
     const uint64_t cbase = (uint64_t)mrow0 * mw;
-    if (tid < nb) {
-        const uint64_t g = b0 + tid;
-        a.mask[g] = msk;
-        const int64_t pg = dc_pred_index(g);
-        int prev = 0;
-        if (pg >= (int64_t)b0) prev = lds.zz[(pg - b0) * kZzStride];
-        else if (pg >= 0) prev = a.coef[(uint64_t)pg * 64];
+    if (blk < nb) {
+        const uint64_t g = b0 + blk;
         const int k = (int)(g % 6);
-        const uint64_t m = g / 6;
-        const uint32_t mrow = (uint32_t)(m / mw), mcol = (uint32_t)(m % mw);
-        uint32_t rel;  // position of this block in its symbol text, relative to the tile base
-        int tdc, tac;
+        const uint64_t m6 = g / 6;
+        const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
+        uint32_t rel;  // index of this block in its symbol text, relative to the tile base
+        int tsel;
         if (k < 4) {
             rel = (uint32_t)((2ull * mrow + (k >> 1)) * (2ull * mw) + 2ull * mcol + (k & 1) - ybase);
-            tdc = 0; tac = 1;
+            tsel = 0;
         } else {
-            rel = (uint32_t)(m - cbase) | (k == 5 ? 0x80000000u : 0u);  // all Cr after all Cb
-            tdc = 2; tac = 3;
+            rel = (uint32_t)(m6 - cbase) | (k == 5 ? 0x80000000u : 0u);  // all Cr after all Cb
+            tsel = 1;
+        }
+        const int16_t* zb = &lds.zz[blk * kZzStride];
+        const uint64_t mask = lds.bmask[blk];
+        if (part == 0) {  // DC symbol (difference to the chain predecessor)
+            const int64_t pg = dc_pred_index(g);
+            int prev = 0;
+            if (pg >= (int64_t)b0) prev = lds.zz[(pg - b0) * kZzStride];
+            else if (pg >= 0) prev = a.coef[(uint64_t)pg * 64];
+            const int dcat = category(zb[0] - prev);
+            atomicAdd(&lds.dcnt[tsel][dcat], 1u);
+            uint32_t* kp = &lds.key[2 * tsel][dcat];
+            if (rel < *kp) atomicMin(kp, rel);
         }
         const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
-        const int dcat = category(dc - prev);
-        atomicAdd(&lds.cnt[tdc][dcat], 1u);
-        atomicMin(&lds.key[tdc][dcat], rel);
-        const int16_t* zb = &lds.zz[tid * kZzStride];
-        uint64_t mm = msk;
-        int last = 0;
-        while (mm) {
-            const int p = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            const int run = p - last - 1;
-            last = p;
+        uint32_t* cnt = lds.acnt[(tid >> 2) & (kHistCopies - 1)][tsel];
+        uint32_t* key = lds.key[2 * tsel + 1];
+        Share sh;
+        sh.init(mask, part);
+        for (int i = 0; i < sh.cnt; ++i) {
+            const int p = __builtin_ctzll(sh.m);
+            sh.m &= sh.m - 1;
+            const int run = p - sh.last - 1;
+            sh.last = p;
             const int sym = ((run & 15) << 4) | category(zb[p]);
-            atomicAdd(&lds.cnt[tac][sym], 1u);
-            atomicMin(&lds.key[tac][sym], acb + 2u * p + 1u);
+            atomicAdd(&cnt[sym], 1u);
+            const uint32_t kk = acb + 2u * p + 1u;
+            if (kk < key[sym]) atomicMin(&key[sym], kk);
             if (run >= 16) {
-                atomicAdd(&lds.cnt[tac][0xF0], (uint32_t)(run >> 4));
-                atomicMin(&lds.key[tac][0xF0], acb + 2u * p);
+                atomicAdd(&cnt[0xF0], (uint32_t)(run >> 4));
+                if (kk - 1u < key[0xF0]) atomicMin(&key[0xF0], kk - 1u);
             }
         }
-        if (last < 63) {  // EOB
-            atomicAdd(&lds.cnt[tac][0], 1u);
-            atomicMin(&lds.key[tac][0], acb + 127u);
+        if (part == kPartsPerBlock - 1 && !(mask >> 63)) {  // EOB
+            atomicAdd(&cnt[0], 1u);
+            if (acb + 127u < key[0]) atomicMin(&key[0], acb + 127u);
         }
     }
     __syncthreads();
@@ -362,11 +442,16 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     const uint64_t ncb = a.g.nmcu();
     for (int i = tid; i < 1024; i += kK2Threads) {
         const int t = i >> 8, s = i & 255;
-        const uint32_t c = lds.cnt[t][s];
+        const bool ac = t & 1;
+        uint32_t c = 0;
+        if (ac) {
+            for (int cp = 0; cp < kHistCopies; ++cp) c += lds.acnt[cp][t >> 1][s];
+        } else if (s < 16) {
+            c = lds.dcnt[t >> 1][s];
+        }
         if (!c) continue;
         atomicAdd(&a.hist.cnt[(rep * 4 + t) * 256 + s], c);
         const uint32_t k32 = lds.key[t][s];
-        const bool ac = t & 1;
         uint64_t base;
         if (t < 2) base = ybase;
         else base = (k32 & 0x80000000u) ? ncb + cbase : cbase;
@@ -378,7 +463,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
 }
 
 // ===========================================================================
-// K3 — entropy coding with two decoupled look-back scans
+// K3 — entropy coding with two decoupled look-back scans (4 lanes per block)
 // ===========================================================================
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
 constexpr uint32_t kSpinLimit = 1u << 22;
@@ -421,7 +506,7 @@ __device__ uint64_t lookback_wave(uint64_t* rec, uint32_t tile, uint64_t agg, ui
                 if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
             continue;
         }
         excl += wave_sum64(lane <= first ? (r & kValMask) : 0ull);
@@ -432,14 +517,16 @@ __device__ uint64_t lookback_wave(uint64_t* rec, uint32_t tile, uint64_t agg, ui
     return excl;
 }
 
-// MSB-first bit sink over big-endian 32-bit LDS words; a thread's first and last
-// words may be shared with its neighbours, so every word is OR-ed in.
+// MSB-first bit sink over big-endian 32-bit words (LDS, or the global fallback
+// slot); a lane's first and last words may be shared with its neighbours, so
+// every word is OR-ed in.
+template <typename W>
 struct BitSink {
-    uint32_t* st;
+    W* st;
     uint32_t word;
     int fill;      // bits placed in the current word (leading bits belong to others)
     uint64_t acc;  // right-aligned pending bits of the current word
-    __device__ __forceinline__ void init(uint32_t* s, uint32_t pos) {
+    __device__ __forceinline__ void init(W* s, uint32_t pos) {
         st = s; word = pos >> 5; fill = (int)(pos & 31); acc = 0;
     }
     __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
@@ -456,126 +543,106 @@ struct BitSink {
     }
 };
 
-__device__ __forceinline__ uint32_t stage_byte(const uint32_t* st, uint32_t i) {
+template <typename W>
+__device__ __forceinline__ uint32_t stage_byte(const W* st, uint32_t i) {
     return (st[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
 }
 
-constexpr int kK3Threads = kEntropyTile;
-constexpr int kStageWords = kEntropyTile * kStageBytesPerBlock / 4 + 2;
+constexpr int kK3Threads = kEntropyTile * kPartsPerBlock;
+constexpr int kK3Waves = kK3Threads / 64;
+constexpr int kStageCapBytes = kEntropyTile * 96;  // typical tiles; larger ones use the global slot
 constexpr int kOutLdsBytes = kEntropyTile * kZzStride * 2;
 
-__global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
-    __shared__ int16_t zz[kEntropyTile * kZzStride];  // reused as the stuffed-output buffer
-    __shared__ uint32_t stage[kStageWords];
-    __shared__ uint32_t tab[4 * 256];
-    __shared__ uint32_t wsum[kK3Threads / 64];
-    __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_prefix, s_ffprefix;
+struct EntropyShare {
+    const int16_t* zb;
+    const uint32_t* tdc;
+    const uint32_t* tac;
+    uint64_t mask;
+    int part, dcdiff;
+    bool active;
+};
 
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
-    for (int i = tid; i < 1024; i += kK3Threads) tab[i] = a.tables[i];
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint32_t nblocks = a.g.nblocks();
-    const uint32_t ntiles = (nblocks + kEntropyTile - 1) / kEntropyTile;
-    const bool last_tile = tile == ntiles - 1;
-    const uint64_t b0 = (uint64_t)tile * kEntropyTile;
-    const int nb = (int)min((uint64_t)kEntropyTile, nblocks - b0);
-    stage_blocks_zz<kK3Threads>(a.coef, b0, nb, zz, tid);
-    __syncthreads();
-
-    const bool active = tid < nb;
-    const uint64_t g = b0 + tid;
-    const int k = (int)(g % 6);
-    uint64_t msk = 0;
-    int dcdiff = 0;
-    const int16_t* zb = &zz[tid * kZzStride];
-    if (active) {
-        msk = a.mask[g];
-        const int64_t pg = dc_pred_index(g);
-        int prev = 0;
-        if (pg >= (int64_t)b0) prev = zz[(pg - b0) * kZzStride];
-        else if (pg >= 0) prev = a.coef[(uint64_t)pg * 64];
-        dcdiff = zb[0] - prev;
-    }
-    const uint32_t* tdc = &tab[(k < 4 ? 0 : 2) * 256];
-    const uint32_t* tac = &tab[(k < 4 ? 1 : 3) * 256];
-
-    // ---- pass 1: bit length of this block ----
+// Bits of this lane's share (DC for part 0, its non-zero run/size symbols, EOB
+// for the last part), computed (pass 1) or emitted (pass 2) in stream order.
+template <bool kEmit, typename W>
+__device__ __forceinline__ uint32_t share_bits(const EntropyShare& e, BitSink<W>* bs) {
+    if (!e.active) return 0;
     uint32_t nbits = 0;
-    if (active) {
-        const int dcat = category(dcdiff);
-        nbits = (tdc[dcat] >> 16) + dcat;
-        const uint32_t zrl = tac[0xF0] >> 16;
-        uint64_t mm = msk;
-        int last = 0;
-        while (mm) {
-            const int p = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            const int run = p - last - 1;
-            last = p;
-            const int cat = category(zb[p]);
-            nbits += (uint32_t)(run >> 4) * zrl + (tac[((run & 15) << 4) | cat] >> 16) + cat;
+    if (e.part == 0) {
+        const int dcat = category(e.dcdiff);
+        const uint32_t ent = e.tdc[dcat];
+        nbits += (ent >> 16) + dcat;
+        if (kEmit) {
+            const uint32_t db = (uint32_t)(e.dcdiff < 0 ? e.dcdiff + (1 << dcat) - 1 : e.dcdiff) & ((1u << dcat) - 1);
+            bs->put(((ent & 0xFFFF) << dcat) | db, (int)(ent >> 16) + dcat);
         }
-        if (last < 63) nbits += tac[0] >> 16;
     }
+    const uint32_t zrl = e.tac[0xF0];
+    Share sh;
+    sh.init(e.mask, e.part);
+    for (int i = 0; i < sh.cnt; ++i) {
+        const int p = __builtin_ctzll(sh.m);
+        sh.m &= sh.m - 1;
+        int run = p - sh.last - 1;
+        sh.last = p;
+        const int v = e.zb[p];
+        const int cat = category(v);
+        if (kEmit) {
+            while (run >= 16) { bs->put(zrl & 0xFFFF, (int)(zrl >> 16)); run -= 16; }
+            const uint32_t ent = e.tac[(run << 4) | cat];
+            const uint32_t vb = (uint32_t)(v < 0 ? v + (1 << cat) - 1 : v) & ((1u << cat) - 1);
+            bs->put(((ent & 0xFFFF) << cat) | vb, (int)(ent >> 16) + cat);
+        } else {
+            nbits += (uint32_t)(run >> 4) * (zrl >> 16) + (e.tac[((run & 15) << 4) | cat] >> 16) + cat;
+        }
+    }
+    if (e.part == kPartsPerBlock - 1 && !(e.mask >> 63)) {  // EOB
+        const uint32_t ent = e.tac[0];
+        nbits += ent >> 16;
+        if (kEmit) bs->put(ent & 0xFFFF, (int)(ent >> 16));
+    }
+    return nbits;
+}
 
-    // ---- tile-local exclusive scan of block lengths ----
-    uint32_t incl = nbits;
+// block-wide exclusive scan of one u32 per thread (thread order)
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* wsum, int lane, int wv, uint32_t& total) {
+    uint32_t incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t o = __shfl_up(incl, d);
         if (lane >= d) incl += o;
     }
+    __syncthreads();
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    uint32_t wbase = 0, total = 0;
+    uint32_t base = 0;
+    total = 0;
 #pragma unroll
-    for (int w = 0; w < kK3Threads / 64; ++w) {
-        if (w < wv) wbase += wsum[w];
-        total += wsum[w];
+    for (int w = 0; w < kK3Waves; ++w) {
+        const uint32_t s = wsum[w];
+        if (w < wv) base += s;
+        total += s;
     }
-    const uint32_t excl_bits = wbase + incl - nbits;
+    return base + incl - v;
+}
 
-    // ---- look-back 1: global bit offset of this tile ----
-    if (wv == 0) {
-        const uint64_t pre = lookback_wave(a.lb_bits, tile, total, a.result + 1, lane);
-        if (lane == 0) s_prefix = pre;
-    }
-    __syncthreads();
-    const uint64_t P = s_prefix;
+template <typename W>
+__device__ __forceinline__ void entropy_tail(const EntropyArgs& a, W* stage, int16_t* zz, uint32_t* wsum,
+                                             uint64_t* s_ffprefix, const EntropyShare& es, uint32_t tile,
+                                             bool last_tile, uint64_t P, uint32_t excl_bits, uint32_t total,
+                                             int tid, int lane, int wv) {
     const uint32_t lead = (uint32_t)(P & 7);
     const uint32_t endbit = lead + total;
     const uint32_t nwords = (endbit + 31) / 32 + 1;
     for (uint32_t i = tid; i < nwords; i += kK3Threads) stage[i] = 0;
     __syncthreads();
 
-    // ---- pass 2: emit (doHuffmanEncoding + MCU concatenation) ----
-    if (active) {
-        BitSink bs;
+    // ---- pass 2: emit (doHuffmanEncoding + MCU concatenation, Image.cpp:737-968) ----
+    {
+        BitSink<W> bs;
         bs.init(stage, lead + excl_bits);
-        const int dcat = category(dcdiff);
-        const uint32_t dce = tdc[dcat];
-        const uint32_t dbits = (uint32_t)(dcdiff < 0 ? dcdiff + (1 << dcat) - 1 : dcdiff) & ((1u << dcat) - 1);
-        bs.put(((dce & 0xFFFF) << dcat) | dbits, (int)(dce >> 16) + dcat);
-        const uint32_t zrl = tac[0xF0];
-        uint64_t mm = msk;
-        int last = 0;
-        while (mm) {
-            const int p = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            int run = p - last - 1;
-            last = p;
-            while (run >= 16) { bs.put(zrl & 0xFFFF, (int)(zrl >> 16)); run -= 16; }
-            const int v = zb[p];
-            const int cat = category(v);
-            const uint32_t e = tac[(run << 4) | cat];
-            const uint32_t vb = (uint32_t)(v < 0 ? v + (1 << cat) - 1 : v) & ((1u << cat) - 1);
-            bs.put(((e & 0xFFFF) << cat) | vb, (int)(e >> 16) + cat);
-        }
-        if (last < 63) { const uint32_t e = tac[0]; bs.put(e & 0xFFFF, (int)(e >> 16)); }
-        bs.flush();
+        share_bits<true>(es, &bs);
+        if (es.active) bs.flush();
     }
     __syncthreads();
 
@@ -596,7 +663,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
                     atomicOr(reinterpret_cast<unsigned long long*>(a.result + 1), 2ull);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(1);
             }
             stage[0] |= (t & 0xFF) << 24;
         }
@@ -609,29 +676,16 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
     const uint32_t lo = min(nown, (uint32_t)tid * per), hi = min(nown, lo + per);
     uint32_t nff = 0;
     for (uint32_t i = lo; i < hi; ++i) nff += stage_byte(stage, i) == 0xFF;
-    uint32_t fincl = nff;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(fincl, d);
-        if (lane >= d) fincl += o;
-    }
-    if (lane == 63) wsum[wv] = fincl;
-    __syncthreads();
-    uint32_t fbase = 0, ftotal = 0;
-#pragma unroll
-    for (int w = 0; w < kK3Threads / 64; ++w) {
-        if (w < wv) fbase += wsum[w];
-        ftotal += wsum[w];
-    }
-    const uint32_t ff_before = fbase + fincl - nff;
+    uint32_t ftotal;
+    const uint32_t ff_before = block_scan(nff, wsum, lane, wv, ftotal);
 
     // ---- look-back 2: stuffed-byte offset ----
     if (wv == 0) {
         const uint64_t pre = lookback_wave(a.lb_ff, tile, ftotal, a.result + 1, lane);
-        if (lane == 0) s_ffprefix = pre;
+        if (lane == 0) *s_ffprefix = pre;
     }
     __syncthreads();
-    const uint64_t D0 = a.hdr_len + (P >> 3) + s_ffprefix;  // first output byte of this tile
+    const uint64_t D0 = a.hdr_len + (P >> 3) + *s_ffprefix;  // first output byte of this tile
     const uint32_t ntot = nown + ftotal + (last_tile ? 2u : 0u);
     if (D0 + ntot > a.out_cap) {
         if (tid == 0) atomicOr(reinterpret_cast<unsigned long long*>(a.result + 1), 4ull);
@@ -677,12 +731,76 @@ __global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
     if (last_tile && tid == 0) a.result[0] = D0 + ntot;
 }
 
+__global__ __launch_bounds__(kK3Threads) void entropy_kernel(EntropyArgs a) {
+    __shared__ int16_t zz[kEntropyTile * kZzStride];  // reused as the stuffed-output buffer
+    __shared__ uint32_t stage[kStageCapBytes / 4 + 2];
+    __shared__ uint32_t tab[4 * 256];
+    __shared__ uint32_t wsum[kK3Waves];
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_prefix, s_ffprefix;
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
+    for (int i = tid; i < 1024; i += kK3Threads) tab[i] = a.tables[i];
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t nblocks = a.g.nblocks();
+    const uint32_t ntiles = (nblocks + kEntropyTile - 1) / kEntropyTile;
+    const bool last_tile = tile == ntiles - 1;
+    const uint64_t b0 = (uint64_t)tile * kEntropyTile;
+    const int nb = (int)min((uint64_t)kEntropyTile, nblocks - b0);
+    stage_blocks_zz<kK3Threads>(a.coef, b0, nb, zz, tid);
+    __syncthreads();
+
+    const int blk = tid / kPartsPerBlock;
+    EntropyShare es;
+    es.part = tid % kPartsPerBlock;
+    es.active = blk < nb;
+    es.zb = &zz[blk * kZzStride];
+    const uint64_t g = b0 + blk;
+    const int k = (int)(g % 6);
+    es.tdc = &tab[(k < 4 ? 0 : 2) * 256];
+    es.tac = &tab[(k < 4 ? 1 : 3) * 256];
+    es.mask = 0;
+    es.dcdiff = 0;
+    if (es.active) {
+        es.mask = a.mask[g];
+        if (es.part == 0) {
+            const int64_t pg = dc_pred_index(g);
+            int prev = 0;
+            if (pg >= (int64_t)b0) prev = zz[(pg - b0) * kZzStride];
+            else if (pg >= 0) prev = a.coef[(uint64_t)pg * 64];
+            es.dcdiff = es.zb[0] - prev;
+        }
+    }
+
+    // ---- pass 1: bit length of this lane's share, tile-local scan ----
+    const uint32_t nbits = share_bits<false, uint32_t>(es, nullptr);
+    uint32_t total;
+    const uint32_t excl_bits = block_scan(nbits, wsum, lane, wv, total);
+
+    // ---- look-back 1: global bit offset of this tile ----
+    if (wv == 0) {
+        const uint64_t pre = lookback_wave(a.lb_bits, tile, total, a.result + 1, lane);
+        if (lane == 0) s_prefix = pre;
+    }
+    __syncthreads();
+    const uint64_t P = s_prefix;
+    const uint32_t need = ((uint32_t)(P & 7) + total + 31) / 32 * 4 + 8;
+    if (need <= min(a.stage_cap, (uint32_t)kStageCapBytes)) {
+        entropy_tail(a, stage, zz, wsum, &s_ffprefix, es, tile, last_tile, P, excl_bits, total, tid, lane, wv);
+    } else {
+        uint32_t* slot = a.scratch + (uint64_t)tile * kScratchWordsPerTile;
+        entropy_tail(a, slot, zz, wsum, &s_ffprefix, es, tile, last_tile, P, excl_bits, total, tid, lane, wv);
+    }
+}
+
 }  // namespace
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
     const uint32_t tiles = ((a.g.mw + 3) / 4) * a.g.mh;
     const uint32_t wgs = (tiles + 3) / 4;
-    const uint32_t grid = wgs < 2048 ? wgs : 2048;
+    const uint32_t grid = wgs < 1024 ? wgs : 1024;  // 4 workgroups per CU, persistent
     if (a.maxval == 255)
         hipLaunchKernelGGL(fdct_kernel<true>, dim3(grid), dim3(kK1Threads), 0, s, a);
     else
@@ -691,7 +809,7 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
-    const uint32_t grid = (a.g.nblocks() + kStatsTile - 1) / kStatsTile;
+    const uint32_t grid = (a.g.nblocks() + kK2Blocks - 1) / kK2Blocks;
     hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(kK2Threads), 0, s, a);
     return hipGetLastError();
 }

@@ -30,9 +30,11 @@ struct Geometry {
 };
 
 constexpr int kHistReplicas = 8;          // spread of the global histogram atomics
-constexpr int kStatsTile = 256;           // blocks per statistics workgroup
-constexpr int kEntropyTile = 128;         // blocks per entropy workgroup
+constexpr int kStatsTile = 128;           // blocks per statistics workgroup (4 lanes each)
+constexpr int kEntropyTile = 128;         // blocks per entropy workgroup (4 lanes each)
 constexpr int kStageBytesPerBlock = 216;  // >= worst-case 1665 bits of one block
+// global fallback staging slot of an entropy tile whose bits exceed the LDS stage
+constexpr uint32_t kScratchWordsPerTile = kEntropyTile * kStageBytesPerBlock / 4 + 8;
 
 // Tables: 0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC.
 struct HistPtrs {
@@ -69,6 +71,8 @@ struct EntropyArgs {
     uint64_t* lb_ff;         // [ntiles] zeroed
     uint32_t* tails;         // [ntiles] zeroed
     uint64_t* result;        // [0] total .jpg bytes, [1] error bits
+    uint32_t* scratch;       // [ntiles][kScratchWordsPerTile] fallback staging
+    uint32_t stage_cap;      // LDS staging bytes to use (0 forces the fallback; tests)
 };
 
 inline uint32_t entropy_tiles(const Geometry& g) {

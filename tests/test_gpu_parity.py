@@ -101,6 +101,22 @@ def test_batch_matches_single(encoder):
         assert o == _oracle.encode(f, 90)
 
 
+@pytest.mark.parametrize("kind,quality", [(0, 90), (1, 100), (2, 50)])
+def test_entropy_global_stage_fallback(kind, quality):
+    # K3 stages each tile's bits in LDS; tiles whose bits exceed it use a global
+    # slot.  Force that path for every tile and check the bytes are unchanged.
+    os.environ["JPGE_FORCE_GLOBAL_STAGE"] = "1"
+    try:
+        enc = J.Encoder(0)
+    finally:
+        del os.environ["JPGE_FORCE_GLOBAL_STAGE"]
+    try:
+        rgb = J.synth_rgb8(31 + kind, 500, 300, kind=kind)
+        assert enc.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
+    finally:
+        enc.close()
+
+
 def test_output_decodes(encoder):
     Image = pytest.importorskip("PIL.Image")
     rgb = J.synth_rgb8(42, 640, 480)
