@@ -17,14 +17,20 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -fopenmp -Wall -Wextra -Wno-unused-parameter -W
 
 HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp
 HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))
-DEV_OBJS  := $(BUILD)/kernels.o
+DEV_SRCS  := fdct.hip stats.hip entropy.hip
+DEV_OBJS  := $(addprefix $(BUILD)/,$(DEV_SRCS:.hip=.o))
+DIAG_OBJS := $(addprefix $(BUILD)/diag/,$(DEV_SRCS:.hip=.o))
 HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h
 
 all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc oracle
 
-$(BUILD)/kernels.o: $(SRC)/kernels.hip $(HEADERS)
+$(BUILD)/%.o: $(SRC)/%.hip $(HEADERS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/diag/%.o: $(SRC)/%.hip $(HEADERS)
+	@mkdir -p $(BUILD)/diag
+	$(HIPCC) $(HIPFLAGS) -DJPGE_STAMPS -c $< -o $@
 
 $(BUILD)/%.o: $(SRC)/%.cpp $(HEADERS)
 	@mkdir -p $(BUILD)
@@ -41,6 +47,13 @@ $(BINDIR)/jpgenc: $(SRC)/cli.cpp $(LIBDIR)/libjpge.so
 
 oracle:
 	$(MAKE) -C oracle
+
+# diagnostic build with in-kernel phase stamps (JPGE_LIB=jpgenc_amd/lib/diag/libjpge.so,
+# JPGE_STAMPS_FILE=<path>); never used by tests or the bench
+diag: $(DIAG_OBJS) $(HOST_OBJS)
+	@mkdir -p $(LIBDIR)/diag
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fopenmp -o $(LIBDIR)/diag/libjpge.so $^ \
+	  -L$(ROCM)/lib -lamdhip64
 
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR)

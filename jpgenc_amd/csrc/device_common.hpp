@@ -1,0 +1,291 @@
+// Device helpers shared by the jpge kernels (fdct.hip, stats.hip, entropy.hip).
+// Included only by HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace jpge {
+namespace dev {
+
+// Diagnostic phase stamps (JPGE_STAMPS builds only; otherwise they compile to
+// nothing): thread 0 of each workgroup records s_memrealtime (100 MHz, chip-wide)
+// at phase boundaries into a.dbg[blockIdx.x * kStampSlots + i] (slots 0-7), and
+// accumulated sub-phase durations into slots 8-15 (JPGE_ACC).  Never part of an
+// output.
+#ifdef JPGE_STAMPS
+#define JPGE_NOW() __builtin_amdgcn_s_memrealtime()
+#define JPGE_STAMP(i)                                                                                    \
+    do {                                                                                                 \
+        if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * kStampSlots + (i)] = JPGE_NOW();              \
+    } while (0)
+#define JPGE_ACC(i, t)                                                                                   \
+    do {                                                                                                 \
+        const uint64_t now_ = JPGE_NOW();                                                                \
+        if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * kStampSlots + 8 + (i)] += now_ - (t);        \
+        (t) = now_;                                                                                      \
+    } while (0)
+#else
+#define JPGE_NOW() 0ull
+#define JPGE_STAMP(i) \
+    do {              \
+    } while (0)
+#define JPGE_ACC(i, t) \
+    do {               \
+        (void)(t);     \
+    } while (0)
+#endif
+
+// natural (row-major) index -> zig-zag position (inverse of Coding.hpp:57-81)
+static __constant__ uint8_t kNatToZz[64] = {
+    0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42,
+    3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24, 31, 40, 44, 53,
+    10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+    21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+// Orders LDS traffic between lanes of ONE wavefront (a wave's DS ops execute in
+// order; this stops the compiler from moving them across the point).
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// getCategoryAndCode, Coding.hpp:197-230: bit length of |v| (0 for v == 0)
+__device__ __forceinline__ int category(int v) {
+    const int av = v < 0 ? -v : v;
+    return av ? 32 - __builtin_clz((unsigned)av) : 0;
+}
+
+constexpr int kZzStride = 72;      // int16 per staged block in LDS (144 B: spreads banks)
+constexpr int kPartsPerBlock = 4;  // lanes cooperating on one block's non-zero coefficients
+
+// DC predecessor of flat block g (Image.cpp:638-678): the Y chain runs in MCU
+// order, Cb and Cr each over their own blocks; a chain's first block predicts 0.
+// The predecessor is at most 6 blocks back.
+__device__ __forceinline__ int64_t dc_pred_index(uint64_t g) {
+    const int k = (int)(g % 6);
+    if (k >= 1 && k <= 3) return (int64_t)g - 1;
+    if (g < 6) return -1;
+    return (int64_t)g - (k == 0 ? 3 : 6);
+}
+
+// One tile of kBlocks coefficient blocks (natural order in HBM) held in registers
+// between its load and its LDS staging, so a persistent workgroup can fetch tile
+// t+1 while it codes tile t.  Lane q of the tile carries row q&7 of block q>>3;
+// lanes < 6 also carry the DC of the 6 blocks before the tile (DC predecessors).
+// The zig-zag positions of a lane's row (row = tid & 7 for every tile) are read
+// from the constant table once, into registers: a global load inside the tile loop
+// would make the in-order vmcnt wait for it also wait for the prefetched tile.
+template <int kThreads, int kBlocks>
+struct TileRegs {
+    static constexpr int kPer = kBlocks * 8 / kThreads;
+    static_assert(kPer * kThreads == kBlocks * 8 && kThreads % 8 == 0, "tile rows must divide over the threads");
+    uint4 v[kPer];
+    int prev_dc;
+    uint32_t zlo, zhi;  // zig-zag positions of this lane's row, 4 per word
+
+    __device__ __forceinline__ void init(int tid) {
+        const uint32_t* z = reinterpret_cast<const uint32_t*>(&kNatToZz[(tid & 7) * 8]);
+        zlo = z[0];
+        zhi = z[1];
+    }
+
+    __device__ __forceinline__ void load(const int16_t* __restrict__ coef, uint64_t b0, int nb, int tid) {
+        const uint4* src = reinterpret_cast<const uint4*>(coef + b0 * 64);
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int q = tid + i * kThreads;
+            v[i] = q < nb * 8 ? src[q] : make_uint4(0, 0, 0, 0);
+        }
+        prev_dc = (tid < 6 && b0 >= 6) ? coef[(b0 - 6 + tid) * 64] : 0;
+    }
+
+    // zig-zag-ordered LDS blocks, the AC non-zero mask of every block (bit p =
+    // zig-zag position p, OR-reduced over the 8 lanes of the block) and the DCs of
+    // the 6 blocks before the tile (prevdc[i] = DC of block b0 - 6 + i)
+    __device__ __forceinline__ void stage(int nb, int16_t* zz, uint64_t* bmask, int* prevdc, int tid) const {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int q = tid + i * kThreads;
+            const bool ok = q < nb * 8;
+            const int blk = q >> 3, row = q & 7;
+            uint64_t m = 0;
+            if (ok) {
+                int16_t* d = zz + blk * kZzStride;
+                const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
+                    const uint32_t zp = ((u < 4 ? zlo : zhi) >> (8 * (u & 3))) & 0xFF;
+                    d[zp] = c;
+                    m |= (uint64_t)(c != 0) << zp;
+                }
+            }
+            m |= __shfl_xor(m, 1);
+            m |= __shfl_xor(m, 2);
+            m |= __shfl_xor(m, 4);
+            if (ok && row == 0) bmask[blk] = m & ~1ull;  // AC only
+        }
+        if (tid < 6) prevdc[tid] = prev_dc;
+    }
+};
+
+// DC of the chain predecessor of block b0+blk (0 for a chain's first block), from
+// the staged tile or the 6 DCs staged before it.
+__device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, const int* prevdc) {
+    const int64_t pg = dc_pred_index(b0 + blk);
+    if (pg < 0) return 0;
+    if (pg >= (int64_t)b0) return zz[(pg - (int64_t)b0) * kZzStride];
+    return prevdc[pg - ((int64_t)b0 - 6)];
+}
+
+// Wait for this lane's outstanding global stores (so a following barrier publishes
+// them to the rest of the workgroup).
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Lane mapping of the symbol kernels (K2, K3): a 512-thread workgroup codes a
+// tile of 128 blocks; wave w covers zig-zag positions [16q, 16q+16), q = w & 3
+// (the "part"), of the 64 blocks (w >> 2) * 64 + lane.  All lanes of a wave visit
+// the same positions, so a position no lane has a non-zero at is skipped by the
+// whole wave.  Stream order of the parts is block-major: index blk * 4 + part.
+__device__ __forceinline__ int part_of(int wv) { return wv & 3; }
+__device__ __forceinline__ int block_of(int wv, int lane) { return (wv >> 2) * 64 + lane; }
+
+struct PartView {
+    uint32_t m16;        // AC non-zero bits of the part's 16 positions (bit i = position 16*part + i)
+    int last;            // zig-zag position of the last non-zero before the part (0 = DC)
+    const int16_t* row;  // the part's 16 staged coefficients (LDS)
+
+    __device__ __forceinline__ void load(const int16_t* zz, uint64_t mask, int blk, int part, bool active) {
+        row = zz + blk * kZzStride + 16 * part;
+        if (!active) mask = 0;
+        m16 = (uint32_t)(mask >> (16 * part)) & 0xFFFFu;
+        const uint64_t below = part ? mask & ((1ull << (16 * part)) - 1) : 0ull;
+        last = below ? 63 - __builtin_clzll(below) : 0;
+    }
+};
+
+// f(p, run, v) for every non-zero AC coefficient of the part, in zig-zag order
+// (run = zeros since the previous non-zero of the block, may be >= 16).  A wave
+// iterates max-over-lanes popcount(m16) times.
+template <typename F>
+__device__ __forceinline__ void for_each_ac(const PartView& pv, int part, F&& f) {
+    uint32_t m = pv.m16;
+    int last = pv.last;
+    while (__ballot(m != 0)) {
+        if (m) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1;
+            const int p = 16 * part + i;
+            f(p, p - last - 1, (int)pv.row[i]);
+            last = p;
+        }
+    }
+}
+
+// ---- inter-workgroup primitives (MI355X_MICROARCH.md, "R2" granules) ----
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// Decoupled look-back.  Records are self-contained 8-byte {flag, value} granules
+// written by one relaxed agent-scope store each, so no payload fence is needed.
+// lookback_publish makes this id's aggregate visible (as early as possible);
+// lookback_resolve, run by one whole wave, inspects kDepth*64 predecessors per
+// pass (kDepth loads in flight per lane) and returns the exclusive prefix.
+__device__ __forceinline__ void lookback_publish(uint64_t* rec, uint32_t id, uint64_t agg, int lane) {
+    if (lane == 0) st_relaxed(&rec[id], (id == 0 ? kFlagIncl : kFlagAgg) | agg);
+}
+
+template <int kDepth>
+__device__ uint64_t lookback_resolve(uint64_t* rec, uint32_t id, uint64_t agg, uint64_t* err, int lane) {
+    if (id == 0) return 0;
+    uint64_t excl = 0;
+    int64_t end = id;
+    uint32_t spins = 0;
+    for (;;) {
+        uint64_t r[kDepth];
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) {  // window position 64k + lane (0 = nearest)
+            const int64_t idx = end - 1 - lane - 64 * k;
+            r[k] = idx >= 0 ? ld_relaxed(&rec[idx]) : kFlagIncl;
+        }
+        int first = 64 * kDepth;
+        bool waiting = false;
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) {
+            const uint64_t f = r[k] & ~kValMask;
+            const uint64_t incl = __ballot(f == kFlagIncl);
+            const uint64_t notready = __ballot(f == 0);
+            if (first == 64 * kDepth) {  // positions up to the nearest inclusive record must be ready
+                const int lim = incl ? __builtin_ctzll(incl) : 63;
+                if (notready & (lim >= 63 ? ~0ull : ((2ull << lim) - 1))) waiting = true;
+                if (incl) first = 64 * k + __builtin_ctzll(incl);
+            }
+        }
+        if (waiting) {
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) v += (64 * k + lane <= first) ? (r[k] & kValMask) : 0ull;
+        excl += wave_sum64(v);
+        if (first < 64 * kDepth) break;
+        end -= 64 * kDepth;
+    }
+    if (lane == 0) st_relaxed(&rec[id], kFlagIncl | (excl + agg));
+    return excl;
+}
+
+template <int kDepth>
+__device__ uint64_t lookback_wave(uint64_t* rec, uint32_t id, uint64_t agg, uint64_t* err, int lane) {
+    lookback_publish(rec, id, agg, lane);
+    return lookback_resolve<kDepth>(rec, id, agg, err, lane);
+}
+
+// block-wide exclusive scan of one u32 per thread (thread order)
+template <int kWaves>
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* wsum, int lane, int wv, uint32_t& total) {
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const uint32_t s = wsum[w];
+        if (w < wv) base += s;
+        total += s;
+    }
+    return base + incl - v;
+}
+
+}  // namespace dev
+}  // namespace jpge

@@ -2,7 +2,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <vector>
 
 namespace jpge {
 
@@ -55,21 +57,16 @@ struct Encoder::Slot {
     size_t cap_mcu = 0, cap_in = 0, cap_out = 0, cap_ctl = 0;
     uint8_t* d_in = nullptr;
     int16_t* d_coef = nullptr;
-    uint64_t* d_mask = nullptr;
     uint8_t* d_ctl = nullptr;
-    uint32_t* d_scratch = nullptr;
-    size_t cap_scratch = 0;
+    uint8_t* d_ubuf = nullptr;  // unstuffed entropy-coded segment (K3 internal)
+    size_t cap_ubuf = 0;
     uint8_t* d_out = nullptr;
-    double* d_q = nullptr;
     uint32_t* d_tab = nullptr;
     // pinned host staging
     HostHist* h_hist = nullptr;
     uint32_t* h_tab = nullptr;
     uint8_t* h_hdr = nullptr;
     uint64_t* h_result = nullptr;
-    double* h_q = nullptr;
-    uint8_t last_q[128] = {0};
-    bool q_valid = false;
     // per-frame state between phases
     const uint8_t* in_dev = nullptr;
     size_t in_stride = 0;
@@ -79,9 +76,9 @@ struct Encoder::Slot {
     uint8_t qy[64], qc[64];
 
     ~Slot() {
-        hipFree(d_in); hipFree(d_coef); hipFree(d_mask); hipFree(d_ctl); hipFree(d_scratch);
-        hipFree(d_out); hipFree(d_q); hipFree(d_tab);
-        hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_hdr); hipHostFree(h_result); hipHostFree(h_q);
+        hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
+        hipFree(d_out); hipFree(d_tab);
+        hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_hdr); hipHostFree(h_result);
         for (auto& e : ev) if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
     }
@@ -101,8 +98,13 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     JPGE_HIP(hipSetDevice(device));
     std::unique_ptr<Encoder> e(new Encoder());
     e->device_ = device;
-    const char* fg = std::getenv("JPGE_FORCE_GLOBAL_STAGE");
-    e->force_global_stage_ = fg && fg[0] == '1';
+    if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
+    e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
+    if (e->stamps_file_) {
+        e->dbg_words_ = 3ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel
+        JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
+        JPGE_HIP(hipMemset(e->d_dbg_, 0, e->dbg_words_ * 8));
+    }
     for (int i = 0; i < 3; ++i) {
         std::unique_ptr<Slot> s(new Slot());
         JPGE_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
@@ -111,8 +113,6 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
         JPGE_HIP(hipHostMalloc((void**)&s->h_tab, 4 * 256 * 4, hipHostMallocDefault));
         JPGE_HIP(hipHostMalloc((void**)&s->h_hdr, 4096, hipHostMallocDefault));
         JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocDefault));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_q, 128 * 8, hipHostMallocDefault));
-        JPGE_HIP(hipMalloc((void**)&s->d_q, 128 * 8));
         JPGE_HIP(hipMalloc((void**)&s->d_tab, 4 * 256 * 4));
         e->slots_.push_back(std::move(s));
     }
@@ -124,23 +124,39 @@ Encoder::~Encoder() {
     hipSetDevice(device_);
     for (auto& s : slots_) if (s && s->stream) hipStreamSynchronize(s->stream);
     slots_.clear();
+    hipFree(d_dbg_);
+}
+
+// Diagnostic: raw per-workgroup phase stamps of the last frame, as
+// [u64 n_fdct_wg, n_stats_wg, n_entropy_wg] then 3 x 65536 x kStampSlots u64;
+// the buffer is cleared afterwards (slots 8-15 accumulate).
+void Encoder::dump_stamps(const Slot& s) {
+    if (!stamps_file_ || !d_dbg_) return;
+    std::vector<uint64_t> h(dbg_words_);
+    if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    const uint64_t hdr[3] = {fdct_grid(s.g), stats_grid(s.g), entropy_grid(s.g, entropy_wgs_)};
+    FILE* f = std::fopen(stamps_file_, "wb");
+    if (!f) return;
+    std::fwrite(hdr, 8, 3, f);
+    std::fwrite(h.data(), 8, h.size(), f);
+    std::fclose(f);
+    hipMemset(d_dbg_, 0, dbg_words_ * 8);
 }
 
 int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap) {
     const size_t nmcu = g.nmcu();
     if (nmcu > s.cap_mcu) {
-        hipFree(s.d_coef); hipFree(s.d_mask);
-        s.d_coef = nullptr; s.d_mask = nullptr; s.cap_mcu = 0;
+        hipFree(s.d_coef);
+        s.d_coef = nullptr; s.cap_mcu = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_coef, nmcu * 768));
-        JPGE_HIP(hipMalloc((void**)&s.d_mask, nmcu * 6 * 8));
         s.cap_mcu = nmcu;
     }
     const CtlLayout L(entropy_tiles(g));
-    const size_t scratch = (size_t)entropy_tiles(g) * kScratchWordsPerTile * 4;
-    if (scratch > s.cap_scratch) {
-        hipFree(s.d_scratch); s.d_scratch = nullptr; s.cap_scratch = 0;
-        JPGE_HIP(hipMalloc((void**)&s.d_scratch, scratch));
-        s.cap_scratch = scratch;
+    const size_t ubuf = entropy_ubuf_bytes(g, entropy_wgs_);
+    if (ubuf > s.cap_ubuf) {
+        hipFree(s.d_ubuf); s.d_ubuf = nullptr; s.cap_ubuf = 0;
+        JPGE_HIP(hipMalloc((void**)&s.d_ubuf, ubuf));
+        s.cap_ubuf = ubuf;
     }
     if (L.total > s.cap_ctl) {
         hipFree(s.d_ctl); s.d_ctl = nullptr; s.cap_ctl = 0;
@@ -160,22 +176,6 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     return kOk;
 }
 
-int Encoder::upload_tables(Slot& s, const uint8_t qy[64], const uint8_t qc[64]) {
-    if (s.q_valid && !std::memcmp(s.last_q, qy, 64) && !std::memcmp(s.last_q + 64, qc, 64)) return kOk;
-    for (int i = 0; i < 64; ++i) {
-        if (!qy[i] || !qc[i]) return kErrArg;
-        s.h_q[i] = (double)qy[i];
-        s.h_q[64 + i] = (double)qc[i];
-    }
-    JPGE_HIP(hipMemcpyAsync(s.d_q, s.h_q, 128 * 8, hipMemcpyHostToDevice, s.stream));
-    // the pinned staging buffer must not be rewritten before the copy ran
-    JPGE_HIP(hipStreamSynchronize(s.stream));
-    std::memcpy(s.last_q, qy, 64);
-    std::memcpy(s.last_q + 64, qc, 64);
-    s.q_valid = true;
-    return kOk;
-}
-
 // Phase 1: upload (if host input), statistics kernels, histogram read-back.
 int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
     if (!f.rgb || f.width == 0 || f.height == 0 || f.width > 65535 || f.height > 65535) return kErrArg;
@@ -187,9 +187,9 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     const size_t dev_pitch = align_up(row, 16);
     const size_t in_bytes = (flags & kFlagDeviceInput) ? 0 : dev_pitch * f.height;
     const size_t out_cap = (flags & kFlagDeviceOutput) ? 0 : max_jpeg_bytes(f.width, f.height);
-    int st = ensure(s, g, in_bytes, out_cap);
-    if (st) return st;
-    st = upload_tables(s, qy, qc);
+    for (int i = 0; i < 64; ++i)
+        if (!qy[i] || !qc[i]) return kErrArg;
+    const int st = ensure(s, g, in_bytes, out_cap);
     if (st) return st;
     std::memcpy(s.qy, qy, 64);
     std::memcpy(s.qc, qc, 64);
@@ -217,14 +217,18 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     a.stride = s.in_stride;
     a.g = g;
     a.maxval = f.maxval;
-    a.qtab = s.d_q;
+    for (int i = 0; i < 64; ++i) {
+        a.q[i] = (double)qy[i];  // Image.cpp:611-636 divides by the table entry as double
+        a.q[64 + i] = (double)qc[i];
+    }
     a.coef = s.d_coef;
+    a.dbg = d_dbg_;
     StatsArgs st2;
     st2.coef = s.d_coef;
-    st2.mask = s.d_mask;
     st2.g = g;
     st2.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
     st2.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
+    st2.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
     JPGE_HIP(launch_fdct(a, s.stream));
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
@@ -267,7 +271,6 @@ int Encoder::phase2(Slot& s, const FrameDesc& f, uint32_t flags) {
     const CtlLayout L(entropy_tiles(s.g));
     EntropyArgs e;
     e.coef = s.d_coef;
-    e.mask = s.d_mask;
     e.g = s.g;
     e.tables = s.d_tab;
     e.out = s.out_dev;
@@ -278,8 +281,9 @@ int Encoder::phase2(Slot& s, const FrameDesc& f, uint32_t flags) {
     e.lb_ff = reinterpret_cast<uint64_t*>(s.d_ctl + L.lb_ff);
     e.tails = reinterpret_cast<uint32_t*>(s.d_ctl + L.tails);
     e.result = reinterpret_cast<uint64_t*>(s.d_ctl + L.result);
-    e.scratch = s.d_scratch;
-    e.stage_cap = force_global_stage_ ? 0u : 0xFFFFFFFFu;
+    e.ubuf = s.d_ubuf;
+    e.wgs = entropy_wgs_;
+    e.dbg = d_dbg_ ? d_dbg_ + 2 * 65536 * kStampSlots : nullptr;
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
     JPGE_HIP(launch_entropy(e, s.stream));
     if (timing_) JPGE_HIP(hipEventRecord(s.ev[5], s.stream));
@@ -299,6 +303,7 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
         times_.entropy_sum += times_.entropy;
         times_.frames += 1;
     }
+    dump_stamps(s);
     const uint64_t err = s.h_result[1];
     if (err & 4) { f.len = 0; return kErrNoSpace; }
     if (err) return kErrTimeout;

@@ -65,11 +65,14 @@ class Encoder {
     int phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
     int phase2(Slot& s, const FrameDesc& f, uint32_t flags);
     int finish(Slot& s, FrameDesc& f, uint32_t flags);
-    int upload_tables(Slot& s, const uint8_t qy[64], const uint8_t qc[64]);
 
     int device_ = 0;
     bool timing_ = false;
-    bool force_global_stage_ = false;  // JPGE_FORCE_GLOBAL_STAGE=1: exercise the K3 fallback (tests)
+    uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
+    const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
+    uint64_t* d_dbg_ = nullptr;
+    size_t dbg_words_ = 0;
+    void dump_stamps(const Slot& s);
     KernelTimes times_;
     std::vector<std::unique_ptr<Slot>> slots_;
 };

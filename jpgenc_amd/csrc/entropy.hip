@@ -1,0 +1,410 @@
+// K3 entropy_kernel (gfx950): Huffman emission (Image.cpp:737-829) in MCU
+// interleave order (Image.cpp:957-968), 1-fill and 0xFF00 stuffing
+// (BitstreamGeneric.hpp:213-248), EOI (Image.cpp:1003-1005).
+//
+// Persistent: a workgroup takes a ticket w (dynamic, so every predecessor it waits
+// for is already resident) and owns the contiguous tiles [w*T/G, (w+1)*T/G) of
+// 128 blocks (2..kEntropyMaxTilesPerWg tiles; 4 lanes per block).
+//   A   per tile (the next tile loads into registers meanwhile): stage, bit length
+//       of every lane's share, tile scan, emit at the workgroup-LOCAL bit offset
+//       into a big-endian LDS word stage, carry the partial last word to the next
+//       tile, store complete words to this workgroup's private region R.
+//       Publish the workgroup's bit total (look-back record 1).
+//   cnt count the 0xFF bytes the stream would hold at each of the 8 possible byte
+//       alignments (still before the global offset is known).
+//   L1  resolve the bit offset P; b = P & 7 is the alignment.  Publish the split
+//       last byte (tail) for workgroup w+1; take w-1's tail for the split first
+//       byte (a byte belongs to the workgroup holding its last bit); the last
+//       workgroup 1-fills its final byte.
+//   L2  look-back over the 0xFF counts -> stuffed output offset.
+//   C   copy R to the output shifted right by b bits, a 0x00 after every 0xFF,
+//       16 KB of R per round through LDS, aligned 4-byte stores.
+// Global traffic: the coefficients once (HBM), R written once and read twice
+// (L2-resident, workgroup-private lines), the output once.
+#include "device_common.hpp"
+
+namespace jpge {
+namespace {
+using namespace dev;
+
+constexpr int kK3Blocks = kEntropyTile;
+constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
+constexpr int kK3Waves = kK3Threads / 64;
+constexpr int kMaxTiles = kEntropyMaxTilesPerWg;
+constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-case tile + lead
+constexpr int kLbDepth = 4;                                           // 256 records per look-back pass
+constexpr int kWin = 32;                                              // output bytes per lane per round
+constexpr int kWinWords = kWin / 4;
+constexpr int kChunk = kK3Threads * kWin;                             // output bytes per round (pre-stuffing)
+
+struct K3Lds {
+    int16_t zz[kK3Blocks * kZzStride];  // staged tile; phase C: stuffed-output buffer
+    uint32_t stage[kStageWords];        // big-endian bit stage of one tile (all zero between tiles)
+    uint32_t tab[4 * 256];              // (len << 16) | code
+    uint64_t bmask[kK3Blocks];
+    int prevdc[6];
+    uint32_t sbits[kK3Threads];  // bits of every part, stream order; then their offsets
+    uint32_t wsum[kK3Waves];
+    uint32_t cnt8[8];
+    uint32_t wg, carry, split, fill, ftotal;
+    uint64_t prefix, ffprefix;
+};
+// phase C stuffs into zz and stage, which are contiguous
+static_assert(offsetof(K3Lds, stage) == sizeof(int16_t) * kK3Blocks * kZzStride, "zz, stage contiguous");
+static_assert(offsetof(K3Lds, tab) >= 2 * kChunk + 8, "stuffing buffer too small");
+static_assert((uint64_t)kMaxTiles * kK3Blocks * kStageBytesPerBlock + 8 <= kEntropyRegionBytes, "region");
+
+// MSB-first bit sink over big-endian 32-bit LDS words; a lane's first and last
+// words may be shared with its neighbours, so every word is OR-ed in.
+struct BitSink {
+    uint32_t* st;
+    uint32_t word;
+    int fill;      // bits placed in the current word (leading bits belong to others)
+    uint64_t acc;  // right-aligned pending bits of the current word
+    __device__ __forceinline__ void init(uint32_t* s, uint32_t pos) {
+        st = s; word = pos >> 5; fill = (int)(pos & 31); acc = 0;
+    }
+    __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
+        acc = (acc << n) | v;
+        fill += n;
+        if (fill >= 32) {
+            fill -= 32;
+            atomicOr(&st[word++], (uint32_t)(acc >> fill));
+            acc &= (1ull << fill) - 1;
+        }
+    }
+    __device__ __forceinline__ void flush() {
+        if (fill > 0) atomicOr(&st[word], (uint32_t)(acc << (32 - fill)));
+    }
+};
+
+// 0x80 in every byte of the big-endian word y that is 0xFF
+__device__ __forceinline__ uint32_t ff_bytes(uint32_t y) {
+    const uint32_t x = ~y;
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+// 0x80 in bytes [lo, hi) (0 = most significant) of a big-endian word; 0 <= lo, hi <= 4
+__device__ __forceinline__ uint32_t byte_range(int lo, int hi) {
+    const uint32_t ge = lo >= 4 ? 0u : 0xFFFFFFFFu >> (8 * lo);
+    const uint32_t lt = hi >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * hi));
+    return ge & lt & 0x80808080u;
+}
+
+// One lane's part of a block: DC (part 0), the run/size symbols of its 16 zig-zag
+// positions, EOB (part 3) — doHuffmanEncoding, Image.cpp:737-829.
+struct PartCoder {
+    PartView pv;
+    const uint32_t* tdc;
+    const uint32_t* tac;
+    uint64_t mask;
+    int part, dcdiff;
+    bool active;
+};
+
+__device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int nb, int blk, int part) {
+    PartCoder c;
+    c.part = part;
+    c.active = blk < nb;
+    const int k = (int)((b0 + blk) % 6);
+    c.tdc = &L.tab[(k < 4 ? 0 : 2) * 256];
+    c.tac = &L.tab[(k < 4 ? 1 : 3) * 256];
+    c.mask = c.active ? L.bmask[blk] : 0ull;
+    c.pv.load(L.zz, c.mask, blk, part, c.active);
+    // DC difference to the chain predecessor, Image.cpp:638-678
+    c.dcdiff = (c.active && part == 0) ? L.zz[blk * kZzStride] - pred_dc(b0, blk, L.zz, L.prevdc) : 0;
+    return c;
+}
+
+// Bits of the part, counted (pass 1) or emitted (pass 2) in stream order.
+template <bool kEmit>
+__device__ __forceinline__ uint32_t part_bits(const PartCoder& c, BitSink* bs) {
+    uint32_t nbits = 0;
+    if (c.active && c.part == 0) {
+        const int dcat = category(c.dcdiff);
+        const uint32_t ent = c.tdc[dcat];
+        nbits += (ent >> 16) + dcat;
+        if (kEmit) {
+            const uint32_t db = (uint32_t)(c.dcdiff < 0 ? c.dcdiff + (1 << dcat) - 1 : c.dcdiff) & ((1u << dcat) - 1);
+            bs->put(((ent & 0xFFFF) << dcat) | db, (int)(ent >> 16) + dcat);
+        }
+    }
+    const uint32_t zrl = c.tac[0xF0];
+    for_each_ac(c.pv, c.part, [&](int p, int run, int v) {
+        const int cat = category(v);
+        if (kEmit) {
+            while (run >= 16) { bs->put(zrl & 0xFFFF, (int)(zrl >> 16)); run -= 16; }
+            const uint32_t ent = c.tac[(run << 4) | cat];
+            const uint32_t vb = (uint32_t)(v < 0 ? v + (1 << cat) - 1 : v) & ((1u << cat) - 1);
+            bs->put(((ent & 0xFFFF) << cat) | vb, (int)(ent >> 16) + cat);
+        } else {
+            nbits += (uint32_t)(run >> 4) * (zrl >> 16) + (c.tac[((run & 15) << 4) | cat] >> 16) + cat;
+        }
+    });
+    if (c.active && c.part == 3 && !(c.mask >> 63)) {  // EOB
+        const uint32_t ent = c.tac[0];
+        nbits += ent >> 16;
+        if (kEmit) bs->put(ent & 0xFFFF, (int)(ent >> 16));
+    }
+    return nbits;
+}
+
+__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_kernel(EntropyArgs a) {
+    __shared__ K3Lds L;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int blk = block_of(wv, lane), part = part_of(wv);
+    JPGE_STAMP(0);
+    if (tid == 0) {
+        L.wg = atomicAdd(a.ticket, 1u);
+        L.carry = 0;
+        L.split = 0;
+        L.fill = 0;
+    }
+    if (tid < 8) L.cnt8[tid] = 0;
+    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
+    for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
+    __syncthreads();
+    const uint32_t wg = L.wg, G = gridDim.x;
+    const bool last = wg == G - 1;
+    const uint32_t nblocks = a.g.nblocks();
+    const uint32_t ntiles = (nblocks + kK3Blocks - 1) / kK3Blocks;
+    const uint32_t tf = (uint32_t)((uint64_t)wg * ntiles / G);
+    const int ntl = (int)((uint64_t)(wg + 1) * ntiles / G) - (int)tf;  // 1..kMaxTiles (entropy_grid)
+    uint64_t* err = a.result + 1;
+    uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
+    uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
+    auto tile_nb = [&](uint32_t t) { return (int)min((uint64_t)kK3Blocks, nblocks - (uint64_t)t * kK3Blocks); };
+
+    // ---- A: emit every tile at workgroup-local bit offsets into R ----
+    TileRegs<kK3Threads, kK3Blocks> regs;
+    regs.init(tid);
+    regs.load(a.coef, (uint64_t)tf * kK3Blocks, tile_nb(tf), tid);
+    uint32_t wl = 0;  // workgroup-local bit position of the current tile
+    uint64_t tq = JPGE_NOW();
+    for (int lt = 0; lt < ntl; ++lt) {
+        const uint64_t b0 = (uint64_t)(tf + lt) * kK3Blocks;
+        const int nb = tile_nb(tf + lt);
+        __syncthreads();  // previous tile: zz readers done, stage re-zeroed, carry set
+        regs.stage(nb, L.zz, L.bmask, L.prevdc, tid);
+        if (lt + 1 < ntl) regs.load(a.coef, b0 + kK3Blocks, tile_nb(tf + lt + 1), tid);
+        __syncthreads();
+        JPGE_ACC(0, tq);
+        L.sbits[blk * 4 + part] = part_bits<false>(make_coder(L, b0, nb, blk, part), nullptr);
+        __syncthreads();
+        JPGE_ACC(1, tq);
+        uint32_t T;  // scan in stream order (thread tid takes stream index tid)
+        const uint32_t ex = block_scan<kK3Waves>(L.sbits[tid], L.wsum, lane, wv, T);
+        L.sbits[tid] = ex;
+        __syncthreads();
+        JPGE_ACC(2, tq);
+        const uint32_t excl = L.sbits[blk * 4 + part];
+        const uint32_t lead = wl & 31;
+        {
+            const PartCoder pc = make_coder(L, b0, nb, blk, part);  // (re-read: fewer live registers)
+            BitSink bs;
+            bs.init(L.stage, lead + excl);
+            part_bits<true>(pc, &bs);
+            if (pc.active) bs.flush();
+        }
+        __syncthreads();
+        JPGE_ACC(3, tq);
+        const uint32_t ncw = (lead + T) >> 5;  // complete words
+        const uint32_t wbase = wl >> 5;
+        for (uint32_t w = tid; w < ncw; w += kK3Threads) {
+            uint32_t v = L.stage[w];
+            if (w == 0) v |= L.carry;  // partial last word of the previous tile
+            R32[wbase + w] = __builtin_bswap32(v);
+            L.stage[w] = 0;
+        }
+        if (tid == 0) {  // (thread 0 consumed the old carry above)
+            uint32_t v = L.stage[ncw];
+            if (ncw == 0) v |= L.carry;
+            L.carry = v;
+            L.stage[ncw] = 0;
+        }
+        wl += T;
+        JPGE_ACC(4, tq);
+    }
+    const uint32_t Lb = wl;  // this workgroup's bits
+    if (tid == 0 && (Lb & 31)) R32[Lb >> 5] = __builtin_bswap32(L.carry);
+    if (wv == 0) lookback_publish(a.lb_bits, wg, Lb, lane);
+    vm_drain();
+    __syncthreads();
+    JPGE_STAMP(1);
+
+    // ---- cnt: 0xFF bytes of the stream at each byte alignment b ----
+    // Output byte j (b = alignment) = local stream bits [8j - b, 8j - b + 8); byte 0
+    // is split with the predecessor when b != 0, the byte after the last complete
+    // one is the tail or the 1-filled final byte: both counted at the edges below.
+    const uint32_t nwr = (Lb + 31) >> 5;  // words of R
+    auto rword = [&](int64_t m) -> uint32_t {  // big-endian value of R word m (0 outside)
+        return (m >= 0 && m < (int64_t)nwr) ? __builtin_bswap32(R32[m]) : 0u;
+    };
+    // A byte of alignment b is 0xFF iff 8 one-bits start at local bit s = 8j - b:
+    // mark every run start (y), then count the starts with s = -b (mod 8).  Starts
+    // s < 0 (the split byte) do not exist and runs past Lb meet the zero padding,
+    // so exactly the bytes [b ? 1 : 0, nc) are counted.
+    {
+        uint32_t c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t m = tid; m < nwr; m += kK3Threads) {
+            const uint32_t x = rword(m), nx = rword((int64_t)m + 1);
+            uint32_t y = x;  // bit 31-t: stream bits [32m+t, 32m+t+8) are all ones
+#pragma unroll
+            for (int k = 1; k < 8; ++k) y &= __builtin_amdgcn_alignbit(x, nx, 32 - k);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) c8[(8 - r) & 7] += __builtin_popcount(y & (0x80808080u >> r));
+        }
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            uint32_t s = c8[b];
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+            if (lane == 0 && s) atomicAdd(&L.cnt8[b], s);
+        }
+    }
+    JPGE_STAMP(2);
+
+    // ---- L1: global bit offset ----
+    if (wv == 0) {
+        const uint64_t pre = lookback_resolve<kLbDepth>(a.lb_bits, wg, Lb, err, lane);
+        if (lane == 0) L.prefix = pre;
+    }
+    __syncthreads();
+    const uint64_t P = L.prefix;
+    const uint32_t b = (uint32_t)(P & 7);
+    const uint32_t nc = (b + Lb) >> 3;  // complete output bytes
+    const uint32_t eb = (b + Lb) & 7;   // bits in the byte after them
+    JPGE_STAMP(3);
+
+    // ---- edges: tail for w+1, split first byte, 1-fill ----
+    if (tid == 0) {
+        auto rbyte = [&](int64_t j) -> uint32_t { return (j >= 0 && j < 4 * (int64_t)nwr) ? R8[j] : 0u; };
+        uint32_t extra = 0;
+        if (eb) {
+            const uint32_t t = (((rbyte((int64_t)nc - 1) << 8) | rbyte(nc)) >> b) & 0xFF;
+            if (last) {  // Bitstream::fill(), BitstreamGeneric.hpp:243-248
+                L.fill = t | (0xFFu >> eb);
+                extra += L.fill == 0xFF;
+            } else {
+                __hip_atomic_store(&a.tails[wg], 0x80000000u | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (b) {
+            uint32_t t = 0, spins = 0;
+            while (!((t = __hip_atomic_load(&a.tails[wg - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 31)) {
+                if (++spins > kSpinLimit) {
+                    atomicOr(reinterpret_cast<unsigned long long*>(err), 2ull);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            L.split = (t & 0xFF) | (rbyte(0) >> b);
+            extra += L.split == 0xFF;
+        }
+        L.ftotal = L.cnt8[b] + extra;
+    }
+    __syncthreads();
+    const uint32_t ftotal = L.ftotal;
+    JPGE_STAMP(4);
+
+    // ---- L2: stuffed-byte offset ----
+    if (wv == 0) {
+        const uint64_t pre = lookback_wave<kLbDepth>(a.lb_ff, wg, ftotal, err, lane);
+        if (lane == 0) L.ffprefix = pre;
+    }
+    __syncthreads();
+    JPGE_STAMP(5);
+
+    // ---- C: shifted, stuffed copy R -> output ----
+    const uint32_t n_own = nc + ((last && eb) ? 1u : 0u);
+    const uint64_t D0 = a.hdr_len + (P >> 3) + L.ffprefix;
+    const uint64_t ntot = (uint64_t)n_own + ftotal + (last ? 2u : 0u);
+    if (D0 + ntot > a.out_cap) {
+        if (tid == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 4ull);
+        return;
+    }
+    uint8_t* ob = reinterpret_cast<uint8_t*>(L.zz);
+    const uint32_t split = L.split, fill = L.fill;
+    uint64_t d = D0;
+    for (uint32_t c = 0; c < n_own; c += kChunk) {
+        const uint32_t j0 = c + kWin * tid;
+        const uint32_t jhi = min(j0 + kWin, n_own);
+        uint32_t y[kWinWords];
+        uint32_t cff = 0;
+        if (j0 < jhi) {
+            uint32_t prev = rword((int64_t)(j0 / 4) - 1);
+#pragma unroll
+            for (int m = 0; m < kWinWords; ++m) {  // output word = R shifted right by b bits
+                const uint32_t cur = rword((int64_t)(j0 / 4) + m);
+                y[m] = __builtin_amdgcn_alignbit(prev, cur, b);
+                prev = cur;
+            }
+            if (j0 == 0 && b) y[0] = (y[0] & 0x00FFFFFFu) | (split << 24);
+            if (last && eb && n_own - 1 < j0 + kWin) {
+                const uint32_t q = n_own - 1 - j0, sh = 24 - 8 * (q & 3);
+#pragma unroll
+                for (int m = 0; m < kWinWords; ++m)
+                    if ((int)(q >> 2) == m) y[m] = (y[m] & ~(0xFFu << sh)) | (fill << sh);
+            }
+#pragma unroll
+            for (int m = 0; m < kWinWords; ++m) {
+                const int n = min((int)(jhi - j0) - 4 * m, 4);
+                if (n > 0) cff += __builtin_popcount(ff_bytes(y[m]) & byte_range(0, n));
+            }
+        }
+        uint32_t chunk_ff;
+        const uint32_t excl = block_scan<kK3Waves>(cff, L.wsum, lane, wv, chunk_ff);
+        const uint32_t cend = min(c + (uint32_t)kChunk, n_own);
+        const uint32_t align = (uint32_t)(d & 3);
+        if (j0 < jhi) {
+            uint32_t o = align + (j0 - c) + excl;
+#pragma unroll
+            for (int q = 0; q < kWin; ++q) {
+                if (j0 + q < jhi) {
+                    const uint8_t v = (uint8_t)(y[q >> 2] >> (24 - 8 * (q & 3)));
+                    ob[o++] = v;
+                    if (v == 0xFF) ob[o++] = 0;
+                }
+            }
+        }
+        const uint32_t clen = (cend - c) + chunk_ff;
+        __syncthreads();
+        uint8_t* gout = a.out + (d - align);
+        const uint32_t nw = (align + clen + 3) / 4;
+        for (uint32_t w = tid; w < nw; w += kK3Threads) {
+            const uint32_t s = 4 * w, e = s + 4;
+            if (s >= align && e <= align + clen) {
+                *reinterpret_cast<uint32_t*>(gout + s) = *reinterpret_cast<const uint32_t*>(ob + s);
+            } else {
+                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = ob[q];
+            }
+        }
+        d += clen;
+        __syncthreads();  // ob is rewritten by the next round
+    }
+    if (last && tid == 0) {  // EOI, Image.cpp:1003-1005
+        a.out[d] = 0xFF;
+        a.out[d + 1] = 0xD9;
+        a.result[0] = d + 2;
+    }
+    JPGE_STAMP(6);
+}
+
+}  // namespace
+
+// Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size), at least two
+// each when the frame has two tiles (so a workgroup's stream holds >= 8 bits and
+// its split first byte and tail byte differ); 512 = two per CU (LDS, registers).
+uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) {
+    const uint32_t nt = entropy_tiles(g);
+    if (nt <= 1) return 1;
+    const uint32_t lo = (nt + kMaxTiles - 1) / kMaxTiles, hi = nt / 2;
+    const uint32_t want = wgs_override ? wgs_override : 512u;
+    return want < lo ? lo : (want > hi ? hi : want);
+}
+
+hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(entropy_kernel, dim3(entropy_grid(a.g, a.wgs)), dim3(kK3Threads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace jpge

@@ -1,12 +1,14 @@
 // Device-side interface of the jpge HIP kernels (gfx950).  Host code fills
-// these parameter blocks; kernels.hip owns the launch geometry.
+// these parameter blocks; fdct.hip / stats.hip / entropy.hip own the launch
+// geometry.
 //
 // Data layout in HBM (per frame):
 //   rgb   : interleaved RGB8, row pitch `stride` (16-byte aligned pitch/base = fast path)
 //   coef  : int16 [nmcu][6][64]  quantised coefficients, NATURAL order inside a block,
 //           blocks in MCU-interleave order Y00 Y01 Y10 Y11 Cb Cr (= entropy order)
-//   mask  : u64   [nmcu][6]      AC non-zero mask, bit p = zig-zag position p (1..63)
 //   hist  : u32 cnt[kHistReplicas][4][256], u64 key[4][256] (~first-occurrence key)
+//   ubuf  : u8 [G][kEntropyRegionBytes] each entropy workgroup's bit stream before
+//           byte alignment and 0xFF stuffing, written and re-read by that workgroup
 #pragma once
 #include <cstdint>
 
@@ -30,11 +32,11 @@ struct Geometry {
 };
 
 constexpr int kHistReplicas = 8;          // spread of the global histogram atomics
-constexpr int kStatsTile = 128;           // blocks per statistics workgroup (4 lanes each)
-constexpr int kEntropyTile = 128;         // blocks per entropy workgroup (4 lanes each)
+constexpr int kStatsTile = 128;           // blocks per statistics tile (4 lanes each)
+constexpr int kEntropyTile = 128;         // blocks per entropy tile (4 lanes each)
+constexpr int kEntropyMaxTilesPerWg = 4;  // tiles a persistent entropy workgroup may own
 constexpr int kStageBytesPerBlock = 216;  // >= worst-case 1665 bits of one block
-// global fallback staging slot of an entropy tile whose bits exceed the LDS stage
-constexpr uint32_t kScratchWordsPerTile = kEntropyTile * kStageBytesPerBlock / 4 + 8;
+constexpr int kStampSlots = 16;           // diagnostic stamp words per workgroup (JPGE_STAMPS builds)
 
 // Tables: 0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC.
 struct HistPtrs {
@@ -46,37 +48,49 @@ struct FdctArgs {
     const uint8_t* rgb;
     uint64_t stride;
     Geometry g;
-    int maxval;          // 255 -> exact integer colour path
-    const double* qtab;  // [128]: luma then chroma, natural order
+    int maxval;      // 255 -> exact integer colour path
+    double q[128];   // luma then chroma quantisers, natural order
     int16_t* coef;
+    uint64_t* dbg;   // diagnostic phase stamps (JPGE_STAMPS builds), else unused
 };
 
 struct StatsArgs {
     const int16_t* coef;
-    uint64_t* mask;
     Geometry g;
     HistPtrs hist;
+    uint64_t* dbg;
 };
 
 struct EntropyArgs {
     const int16_t* coef;
-    const uint64_t* mask;
     Geometry g;
     const uint32_t* tables;  // [4][256] (len << 16) | code
     uint8_t* out;            // whole .jpg (header already at [0, hdr_len))
     uint64_t hdr_len;
     uint64_t out_cap;
+    uint8_t* ubuf;           // per-workgroup unstuffed regions (entropy_ubuf_bytes)
     uint32_t* ticket;        // zeroed per launch
-    uint64_t* lb_bits;       // [ntiles] zeroed
-    uint64_t* lb_ff;         // [ntiles] zeroed
-    uint32_t* tails;         // [ntiles] zeroed
+    uint64_t* lb_bits;       // [entropy_tiles] zeroed (look-back records, per workgroup)
+    uint64_t* lb_ff;         // [entropy_tiles] zeroed
+    uint32_t* tails;         // [entropy_tiles] zeroed
     uint64_t* result;        // [0] total .jpg bytes, [1] error bits
-    uint32_t* scratch;       // [ntiles][kScratchWordsPerTile] fallback staging
-    uint32_t stage_cap;      // LDS staging bytes to use (0 forces the fallback; tests)
+    uint32_t wgs;            // workgroup count override (0 = automatic; tests)
+    uint64_t* dbg;
 };
 
 inline uint32_t entropy_tiles(const Geometry& g) {
     return (g.nblocks() + kEntropyTile - 1) / kEntropyTile;
+}
+// bytes of one entropy workgroup's private region: its bit stream (workgroup-
+// local offsets, worst case) plus slack, a whole number of 128-byte lines
+constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntropyTile * kStageBytesPerBlock + 128;
+
+uint32_t fdct_grid(const Geometry& g);
+uint32_t stats_grid(const Geometry& g);
+uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override);
+
+inline uint64_t entropy_ubuf_bytes(const Geometry& g, uint32_t wgs_override) {
+    return (uint64_t)entropy_grid(g, wgs_override) * kEntropyRegionBytes;
 }
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s);

@@ -1,0 +1,151 @@
+// K2 stats_kernel (gfx950): DC difference chain (Image.cpp:638-678) + zig-zag RLE
+// + category coding (Coding.hpp:148-283) -> the four symbol histograms of
+// writeJPEG's "texts" (Image.cpp:888-906) with first-occurrence keys.
+//
+// Lane mapping: PartView (device_common.hpp), four lanes per block, one wave per
+// 16 zig-zag positions of 64 blocks.  Persistent grid:
+// each workgroup owns a contiguous run of 128-block tiles (the next one is loaded
+// into registers while the current one is counted), accumulates into LDS
+// (8 copies of the AC counters cap same-address atomics at 8 lanes) and flushes
+// once into kHistReplicas global replicas.  First-occurrence keys (text index of
+// the symbol, see huffman.hpp) are kept workgroup-relative in u32 LDS words and
+// widened at the flush; the global key is stored inverted so atomicMax keeps the
+// minimum.
+#include "device_common.hpp"
+
+namespace jpge {
+namespace {
+using namespace dev;
+
+constexpr int kK2Blocks = kStatsTile;
+constexpr int kK2Threads = kK2Blocks * kPartsPerBlock;
+constexpr int kHistCopies = 8;
+
+struct K2Lds {
+    int16_t zz[kK2Blocks * kZzStride];
+    uint32_t acnt[kHistCopies][2][256];  // AC counters (Y-AC, C-AC), per copy
+    uint32_t dcnt[2][16];                // DC counters (Y-DC, C-DC)
+    uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
+    uint64_t bmask[kK2Blocks];
+    int prevdc[6];
+};
+
+__global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
+    __shared__ K2Lds lds;
+    const int tid = threadIdx.x;
+    const uint32_t nblocks = a.g.nblocks(), mw = a.g.mw;
+    const uint32_t ntiles = (nblocks + kK2Blocks - 1) / kK2Blocks;
+    const uint32_t t_first = (uint32_t)((uint64_t)blockIdx.x * ntiles / gridDim.x);
+    const uint32_t t_last = (uint32_t)((uint64_t)(blockIdx.x + 1) * ntiles / gridDim.x);
+    for (int i = tid; i < kHistCopies * 512; i += kK2Threads) (&lds.acnt[0][0][0])[i] = 0;
+    for (int i = tid; i < 1024; i += kK2Threads) (&lds.key[0][0])[i] = 0xFFFFFFFFu;
+    if (tid < 32) (&lds.dcnt[0][0])[tid] = 0;
+    JPGE_STAMP(0);
+    // key bases: Y raster index of the first Y block row of this workgroup's first
+    // MCU row, chroma raster index of that MCU row (keys are relative to them)
+    const uint32_t mrow0 = (uint32_t)(((uint64_t)t_first * kK2Blocks) / 6) / mw;
+    const uint64_t ybase = 2ull * mrow0 * (2ull * mw);
+    const uint64_t cbase = (uint64_t)mrow0 * mw;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int blk = block_of(wv, lane), part = part_of(wv);
+    auto tile_nb = [&](uint32_t t) { return (int)min((uint64_t)kK2Blocks, nblocks - (uint64_t)t * kK2Blocks); };
+    TileRegs<kK2Threads, kK2Blocks> regs;
+    regs.init(tid);
+    if (t_first < t_last) regs.load(a.coef, (uint64_t)t_first * kK2Blocks, tile_nb(t_first), tid);
+
+    uint64_t tq = JPGE_NOW();
+    for (uint32_t tile = t_first; tile < t_last; ++tile) {
+        const uint64_t b0 = (uint64_t)tile * kK2Blocks;
+        const int nb = tile_nb(tile);
+        __syncthreads();  // previous tile's readers are done with zz / bmask
+        regs.stage(nb, lds.zz, lds.bmask, lds.prevdc, tid);
+        if (tile + 1 < t_last) regs.load(a.coef, b0 + kK2Blocks, tile_nb(tile + 1), tid);
+        __syncthreads();
+        JPGE_STAMP(1);
+        JPGE_ACC(0, tq);
+        const bool active = blk < nb;
+        const uint64_t g = b0 + blk;
+        const int k = (int)(g % 6);
+        const uint64_t m6 = g / 6;
+        const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
+        uint32_t rel;  // index of this block in its symbol text, relative to the bases
+        int tsel;
+        if (k < 4) {
+            rel = (uint32_t)((2ull * mrow + (k >> 1)) * (2ull * mw) + 2ull * mcol + (k & 1) - ybase);
+            tsel = 0;
+        } else {
+            rel = (uint32_t)(m6 - cbase) | (k == 5 ? 0x80000000u : 0u);  // all Cr after all Cb
+            tsel = 1;
+        }
+        const uint64_t mask = lds.bmask[blk];
+        PartView pv;
+        pv.load(lds.zz, mask, blk, part, active);
+        if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
+            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc));
+            atomicAdd(&lds.dcnt[tsel][dcat], 1u);
+            uint32_t* kp = &lds.key[2 * tsel][dcat];
+            if (rel < *kp) atomicMin(kp, rel);
+        }
+        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
+        uint32_t* cnt = lds.acnt[lane & (kHistCopies - 1)][tsel];
+        uint32_t* key = lds.key[2 * tsel + 1];
+        for_each_ac(pv, part, [&](int p, int run, int v) {
+            const int sym = ((run & 15) << 4) | category(v);
+            atomicAdd(&cnt[sym], 1u);
+            const uint32_t kk = acb + 2u * p + 1u;
+            if (kk < key[sym]) atomicMin(&key[sym], kk);
+            if (run >= 16) {
+                atomicAdd(&cnt[0xF0], (uint32_t)(run >> 4));
+                if (kk - 1u < key[0xF0]) atomicMin(&key[0xF0], kk - 1u);
+            }
+        });
+        if (active && part == 3 && !(mask >> 63)) {  // EOB
+            atomicAdd(&cnt[0], 1u);
+            if (acb + 127u < key[0]) atomicMin(&key[0], acb + 127u);
+        }
+        JPGE_ACC(1, tq);
+    }
+    __syncthreads();
+    JPGE_STAMP(2);
+
+    const int rep = blockIdx.x % kHistReplicas;
+    const uint64_t ncb = a.g.nmcu();
+#pragma unroll
+    for (int r = 0; r < 1024 / kK2Threads; ++r) {
+        const int i = tid + r * kK2Threads;
+        const int t = i >> 8, s = i & 255;
+        const bool ac = t & 1;
+        uint32_t c = 0;
+        if (ac) {
+            for (int cp = 0; cp < kHistCopies; ++cp) c += lds.acnt[cp][t >> 1][s];
+        } else if (s < 16) {
+            c = lds.dcnt[t >> 1][s];
+        }
+        if (!c) continue;
+        atomicAdd(&a.hist.cnt[(rep * 4 + t) * 256 + s], c);
+        const uint32_t k32 = lds.key[t][s];
+        uint64_t base;
+        if (t < 2) base = ybase;
+        else base = (k32 & 0x80000000u) ? ncb + cbase : cbase;
+        const uint64_t gkey = (ac ? base * 128ull : base) + (k32 & 0x7FFFFFFFu);
+        const unsigned long long inv = ~gkey;
+        unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[t * 256 + s]);
+        if (inv > *gk) atomicMax(gk, inv);
+    }
+    __syncthreads();
+    JPGE_STAMP(3);
+}
+
+}  // namespace
+
+uint32_t stats_grid(const Geometry& g) {
+    const uint32_t tiles = (g.nblocks() + kK2Blocks - 1) / kK2Blocks;
+    return tiles < 512 ? tiles : 512;  // 2 per CU, persistent over contiguous tiles
+}
+
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(stats_kernel, dim3(stats_grid(a.g)), dim3(kK2Threads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace jpge

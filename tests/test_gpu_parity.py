@@ -101,18 +101,36 @@ def test_batch_matches_single(encoder):
         assert o == _oracle.encode(f, 90)
 
 
-@pytest.mark.parametrize("kind,quality", [(0, 90), (1, 100), (2, 50)])
-def test_entropy_global_stage_fallback(kind, quality):
-    # K3 stages each tile's bits in LDS; tiles whose bits exceed it use a global
-    # slot.  Force that path for every tile and check the bytes are unchanged.
-    os.environ["JPGE_FORCE_GLOBAL_STAGE"] = "1"
+def _encoder_with_wgs(wgs):
+    os.environ["JPGE_ENTROPY_WGS"] = str(wgs)
     try:
-        enc = J.Encoder(0)
+        return J.Encoder(0)
     finally:
-        del os.environ["JPGE_FORCE_GLOBAL_STAGE"]
+        del os.environ["JPGE_ENTROPY_WGS"]
+
+
+# The entropy kernel splits the frame's 128-block tiles into contiguous runs of
+# 2..4 tiles per workgroup; every split must give the same bytes.  Widths of
+# 65 and 129 MCUs leave a final tile of 6 blocks (a few bits).
+@pytest.mark.parametrize("wgs", [1, 3, 5, 100000])
+@pytest.mark.parametrize("w,h,kind,quality", [(500, 300, 0, 90), (500, 300, 1, 100), (500, 300, 2, 50),
+                                              (1040, 16, 0, 75), (2064, 16, 1, 95), (16, 1040, 0, 50),
+                                              (128, 128, 1, 100)])
+def test_entropy_workgroup_partitions(wgs, w, h, kind, quality):
+    enc = _encoder_with_wgs(wgs)
     try:
-        rgb = J.synth_rgb8(31 + kind, 500, 300, kind=kind)
+        rgb = J.synth_rgb8(31 + kind + w, w, h, kind=kind)
         assert enc.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
+    finally:
+        enc.close()
+
+
+@pytest.mark.parametrize("wgs", [1, 100000])
+def test_entropy_workgroup_partitions_4k(wgs):
+    enc = _encoder_with_wgs(wgs)
+    try:
+        rgb = J.synth_rgb8(11, 3840, 2160, kind=1)
+        assert enc.encode(rgb, quality=90) == _oracle.encode(rgb, 90)
     finally:
         enc.close()
 

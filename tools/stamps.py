@@ -1,0 +1,60 @@
+"""Summarise diagnostic phase stamps (diag build, JPGE_STAMPS_FILE) of one frame:
+per kernel, the mean/median duration of each phase per workgroup, the spread of
+workgroup start/end times, and the accumulated per-tile sub-phase durations
+(slots 8-15).  s_memrealtime ticks -> us at --ghz."""
+import argparse
+
+import numpy as np
+
+SLOTS = 16
+PHASES = {
+    "fdct": ["start", "", "", "", "", "", "", "end"],
+    "stats": ["start", "staged", "histogram", "flush", "", "", "", ""],
+    "entropy": ["start", "emit", "count8", "lookback1", "edges", "lookback2", "output", ""],
+}
+ACC = {
+    "stats": ["stage", "count"],
+    "entropy": ["stage", "pass1", "scan", "emit", "store"],
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("file")
+    ap.add_argument("--ghz", type=float, default=0.1)  # s_memrealtime: 100 MHz
+    a = ap.parse_args()
+    raw = np.fromfile(a.file, np.uint64)
+    n = raw[:3].astype(np.int64)
+    data = raw[3:].reshape(3, 65536, SLOTS).astype(np.int64)
+    us = lambda x: x / (a.ghz * 1e3)
+    for k, name in enumerate(["fdct", "stats", "entropy"]):
+        full = data[k, : n[k]]
+        labels = PHASES[name]
+        used = [i for i, l in enumerate(labels) if l]
+        d = full[:, used]
+        keep = (d > 0).all(axis=1)  # launched workgroups only
+        d, full = d[keep], full[keep]
+        if not len(d):
+            continue
+        t0 = d[:, 0].min()
+        starts = np.sort(d[:, 0] - t0)
+        ends = d[:, -1] - t0
+        tm = np.median(np.concatenate([starts, ends]))
+        alive = int(((d[:, 0] - t0 <= tm) & (ends >= tm)).sum())
+        print(f"{name}: alive at median time {alive}; start quantiles (us) "
+              + " ".join(f"{q}:{us(starts[int(q / 100 * (len(starts) - 1))]):.1f}" for q in (0, 25, 50, 75, 100)))
+        print(f"{name}: {n[k]} workgroups, span {us(d[:, -1].max() - t0):.1f} us, "
+              f"start spread {us(d[:, 0].max() - t0):.1f} us")
+        for j in range(1, len(used)):
+            dur = us(d[:, j] - d[:, j - 1])
+            print(f"   {labels[used[j - 1]]:>14s} -> {labels[used[j]]:<14s} mean {dur.mean():7.2f}  "
+                  f"median {np.median(dur):7.2f}  p95 {np.percentile(dur, 95):7.2f} us")
+        life = us(d[:, -1] - d[:, 0])
+        print(f"   workgroup lifetime mean {life.mean():.2f} us, max {life.max():.2f} us")
+        for j, lab in enumerate(ACC.get(name, [])):
+            acc = us(full[:, 8 + j])
+            print(f"   [per-workgroup total] {lab:<8s} mean {acc.mean():7.2f}  p95 {np.percentile(acc, 95):7.2f} us")
+
+
+if __name__ == "__main__":
+    main()
