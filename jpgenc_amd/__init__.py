@@ -17,7 +17,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libjpge.so")
+LIB_PATH = os.environ.get("JPGE_LIB") or os.path.join(_HERE, "lib", "libjpge.so")
 
 JPGE_DEVICE_INPUT = 1
 JPGE_DEVICE_OUTPUT = 2
