@@ -10,9 +10,15 @@ the colour/DCT stage reads from HBM).  Frames are independent, so with N GPUs
 each rank encodes its own F frames (weak scaling, no data-path collective);
 the gloo process group only provides the barriers and the max-over-ranks time.
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (K1,
-HIP-event timed on its own stream inside the timed region) and the CPU
-baseline (the test-only oracle on the host cores, rank 0 at N=1).
+Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel (largest
+HIP-event time per frame on its own stream inside the timed region); `stages`
+carries all three kernels, each with its algorithmic bytes per launch:
+  fdct_kernel    RGB8 read 3 B/px + int16 coefficients written 3 B/px
+  stats_kernel   coefficients read 3 B/px
+  entropy_kernel coefficients read 3 B/px + entropy-coded bytes written
+`traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary
+(profiles/pmc_r01.json, FETCH_SIZE doubled on gfx950).  The CPU baseline is the
+test-only oracle on the host cores, rank 0 at N=1.
 """
 from __future__ import annotations
 
@@ -42,6 +48,9 @@ def parse():
     ap.add_argument("--height", type=int, default=H4K)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket the kernels of every N-th frame with HIP events (each event costs GPU time)")
     return ap.parse_args()
 
 
@@ -117,17 +126,16 @@ def cpu_baseline(args) -> dict:
     }
 
 
-def load_pmc_traffic(profile_dir: str, width: int, height: int):
-    """Per-launch HBM bytes of K1 from the committed rocprofv3 PMC summary."""
-    path = os.path.join(profile_dir, "pmc_fdct.json")
+def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
+    """Per-launch HBM bytes per kernel from the committed rocprofv3 PMC summary."""
     try:
-        with open(path) as f:
+        with open(os.path.join(profile_dir, "pmc_r01.json")) as f:
             d = json.load(f)
         if d.get("width") == width and d.get("height") == height:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+            return {k.split("<")[0]: v["hbm_bytes_per_launch"] for k, v in d["kernels"].items()}
+    except (OSError, ValueError, KeyError):
         pass
-    return None
+    return {}
 
 
 def main():
@@ -163,7 +171,7 @@ def main():
         enc.encode_batch_dev(frames, outd, quality=args.quality)
     torch.cuda.synchronize()
 
-    enc.set_timing(True)
+    enc.set_timing(0 if args.no_kernel_events else args.event_every)
     enc.reset_timing()
     barrier(pg)
     torch.cuda.synchronize()
@@ -182,12 +190,24 @@ def main():
     pixels = sum_over_ranks(pg, float(W * H * F * args.steps))
     value = pixels / dt_max / 1e6
 
-    # roofline of the dominant kernel (K1): algorithmic bytes = 3 B/px RGB read +
-    # 3 B/px int16 coefficients written (1.5 coeff/px at 4:2:0), SURVEY 8(d)
-    k1_ms = tm["fdct_sum"] / max(1, tm["frames"])
-    alg_bytes = 6.0 * W * H
-    achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
+    # per-kernel rooflines (HBM-bound integer/fp64 work; algorithmic bytes per launch)
+    nfr = max(1, tm["frames"])
+    npx = W * H
+    avg_jpeg = total_bytes / (args.steps * F)
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H)
+    stage_defs = [
+        ("fdct_kernel", tm["fdct_sum"] / nfr, 6.0 * npx, "RGB8 read 3 B/px + int16 coefficients written 3 B/px"),
+        ("stats_kernel", tm["dc_stats_sum"] / nfr, 3.0 * npx, "coefficients read 3 B/px"),
+        ("entropy_kernel", tm["entropy_sum"] / nfr, 3.0 * npx + avg_jpeg,
+         "coefficients read 3 B/px + entropy-coded bytes written"),
+    ]
+    stages = {}
+    for name, ms, alg, what in stage_defs:
+        ach = alg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # (0: --no-kernel-events)
+        stages[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
+                        "alg_bytes_per_launch": int(alg), "alg_bytes": what, "avg_kernel_ms": round(ms, 5)}
+    dominant = max(stages, key=lambda k: stages[k]["avg_kernel_ms"])
 
     if rank == 0:
         line = {
@@ -211,22 +231,8 @@ def main():
                 "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
                 "avg_jpeg_bytes": int(total_bytes / (args.steps * F)),
             },
-            "roofline": {
-                "kernel": "fdct_kernel (colour+4:2:0+FDCT+quant+AC stats)",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_launch": int(alg_bytes),
-                "avg_kernel_ms": round(k1_ms, 5),
-            },
-            "stage_ms": {
-                "fdct": round(k1_ms, 5),
-                "dc_stats": round(tm["dc_stats_sum"] / max(1, tm["frames"]), 5),
-                "entropy": round(tm["entropy_sum"] / max(1, tm["frames"]), 5),
-            },
+            "roofline": dict(kernel=dominant, **stages[dominant]),
+            "stages": stages,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)

@@ -70,7 +70,9 @@ int jpge_device_count(int* n);
 /* Context lifetime (replaces nothing in the reference: its encoder is stateless). */
 int jpge_open(int device, jpge_ctx** ctx);
 int jpge_close(jpge_ctx* ctx);
-int jpge_set_timing(jpge_ctx* ctx, int on);
+/* Kernel timing with HIP events on the encoder's stream: every = 0 off, N >= 1
+ * times the kernels of every N-th frame (1 = all; events cost GPU time). */
+int jpge_set_timing(jpge_ctx* ctx, int every);
 int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t);
 int jpge_reset_timing(jpge_ctx* ctx);
 

@@ -226,8 +226,9 @@ class Encoder:
     def ctx(self) -> ctypes.c_void_p:
         return self._ctx
 
-    def set_timing(self, on: bool = True) -> None:
-        _check(lib().jpge_set_timing(self._ctx, int(on)), "set_timing")
+    def set_timing(self, every: int = 1) -> None:
+        """HIP-event kernel timing of every `every`-th frame (0/False = off, True = all)."""
+        _check(lib().jpge_set_timing(self._ctx, int(every)), "set_timing")
 
     def timing(self) -> dict:
         t = Timing()

@@ -71,9 +71,9 @@ int jpge_close(jpge_ctx* ctx) {
     return JPGE_OK;
 }
 
-int jpge_set_timing(jpge_ctx* ctx, int on) {
+int jpge_set_timing(jpge_ctx* ctx, int every) {
     if (!ctx) return JPGE_E_ARG;
-    ctx->enc->set_timing(on != 0);
+    ctx->enc->set_timing(every);
     return JPGE_OK;
 }
 

@@ -1,9 +1,18 @@
 #include "encoder.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+#include <sys/prctl.h>
 #include <vector>
 
 namespace jpge {
@@ -26,9 +35,44 @@ inline Geometry geometry(uint32_t w, uint32_t h) {
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-// Control block zeroed before every frame (Guideline 16: re-initialise every call).
+// Host-side wait with low wake-up latency (the pipeline waits on short intervals).
+inline hipError_t wait_event(hipEvent_t e) {
+    hipError_t r;
+    while ((r = hipEventQuery(e)) == hipErrorNotReady) {
+    }
+    return r;
+}
+
+// Poll a sequence word a kernel writes into mapped host memory after its data
+// (release-ordered).  `nap`: sleep ~10 us between polls (pool workers, which have
+// slack) instead of spinning (the submitting thread).  Bounded: a stream error or
+// ~20 s without progress fails.
+inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool nap = false) {
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 0;; ++spins) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return kOk;
+        if (nap) std::this_thread::sleep_for(std::chrono::microseconds(10));
+        if ((spins & 4095) == 4095 || (nap && (spins & 63) == 63)) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return kErrHip;
+            if (q == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) return kErrInternal;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) return kErrTimeout;
+        }
+    }
+}
+
+constexpr int kSlots = 6;        // frames in flight (device workspaces)
+constexpr int kLookahead = 3;    // frames whose transform is queued ahead of an entropy launch
+constexpr int kDrainLag = 2;     // iterations between an entropy launch and its drain
+constexpr int kTableThreads = 4; // host workers building Huffman tables (one frame each)
+static_assert(kSlots >= kLookahead + kDrainLag + 1, "slot reuse");
+
+constexpr size_t kTabBytes = 4 * 256 * 4;  // code tables as uploaded
+constexpr size_t kHdrMax = 4096;           // headers SOI .. SOS (<= 20 + 2*69 + 19 + 4*277 + 14)
+
+// Control block, zeroed at the start of every frame by the first kernel (K1).
 struct CtlLayout {
-    size_t cnt, key, ticket, lb_bits, lb_ff, tails, result, total;
+    size_t cnt, key, ticket, lb_bits, lb_ff, tails, total;
     explicit CtlLayout(uint32_t ntiles) {
         size_t o = 0;
         cnt = o; o += align_up((size_t)kHistReplicas * 4 * 256 * 4, 256);
@@ -37,21 +81,70 @@ struct CtlLayout {
         lb_bits = o; o += align_up((size_t)ntiles * 8, 256);
         lb_ff = o; o += align_up((size_t)ntiles * 8, 256);
         tails = o; o += align_up((size_t)ntiles * 4, 256);
-        result = o; o += 256;
         total = o;
     }
 };
 
-struct HostHist {
-    uint32_t cnt[kHistReplicas * 4 * 256];
-    uint64_t key[4 * 256];
+struct HostHist {  // written by hist_export_kernel into mapped pinned memory
+    uint32_t cnt[4 * 256];  // replicas summed
+    uint64_t key[4 * 256];  // ~first-occurrence key
+    uint64_t seq;           // frame sequence number, written after the data
 };
 
 }  // namespace
 
+// Host worker threads for the Huffman-table build (package-merge with libstdc++
+// heap order is inherently serial per table, so frames are built side by side).
+class Encoder::TablePool {
+  public:
+    explicit TablePool(int n) {
+        for (int i = 0; i < n; ++i)
+            th_.emplace_back([this] {
+                prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // ~1 us sleeps while polling
+                run();
+            });
+    }
+    ~TablePool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void submit(std::function<void()> job) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(std::move(job));
+        }
+        cv_.notify_one();
+    }
+
+  private:
+    void run() {
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                job = std::move(q_.front());
+                q_.pop_front();
+            }
+            job();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+};
+
 struct Encoder::Slot {
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[6] = {};
+    hipStream_t stream = nullptr;  // the encoder's stream (shared by all slots, not owned)
+    // 0-2, 4-5 kernel timing brackets, 7 output copied to the host (3, 6 unused)
+    hipEvent_t ev[8] = {};
     Geometry g;
     // device workspace (capacities)
     size_t cap_mcu = 0, cap_in = 0, cap_out = 0, cap_ctl = 0;
@@ -61,12 +154,13 @@ struct Encoder::Slot {
     uint8_t* d_ubuf = nullptr;  // unstuffed entropy-coded segment (K3 internal)
     size_t cap_ubuf = 0;
     uint8_t* d_out = nullptr;
-    uint32_t* d_tab = nullptr;
+    uint32_t* d_tab = nullptr;  // [1024] tables, then the header bytes (one upload)
     // pinned host staging
     HostHist* h_hist = nullptr;
-    uint32_t* h_tab = nullptr;
-    uint8_t* h_hdr = nullptr;
-    uint64_t* h_result = nullptr;
+    HostHist* d_hist_host = nullptr;  // device view of h_hist
+    uint32_t* h_tab = nullptr;     // same layout as d_tab
+    uint64_t* h_result = nullptr;  // mapped: written by the entropy kernel's last workgroup
+    uint64_t* d_result_host = nullptr;
     // per-frame state between phases
     const uint8_t* in_dev = nullptr;
     size_t in_stride = 0;
@@ -74,13 +168,16 @@ struct Encoder::Slot {
     size_t out_cap = 0;
     size_t hdr_len = 0;
     uint8_t qy[64], qc[64];
+    bool timed = false;                // this frame's kernels are bracketed by timing events
+    uint64_t seq = 0;                  // frame sequence number (handshakes via mapped memory)
+    std::atomic<int> tables_done{0};   // set by build_tables (any thread)
+    int tables_status = 0;
 
     ~Slot() {
         hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
         hipFree(d_out); hipFree(d_tab);
-        hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_hdr); hipHostFree(h_result);
+        hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_result);
         for (auto& e : ev) if (e) hipEventDestroy(e);
-        if (stream) hipStreamDestroy(stream);
     }
 };
 
@@ -99,21 +196,28 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     std::unique_ptr<Encoder> e(new Encoder());
     e->device_ = device;
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
+    if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     if (e->stamps_file_) {
         e->dbg_words_ = 3ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
         JPGE_HIP(hipMemset(e->d_dbg_, 0, e->dbg_words_ * 8));
     }
-    for (int i = 0; i < 3; ++i) {
+    // One in-order stream for every slot: frame i+1's transform and statistics
+    // kernels are queued ahead of frame i's entropy kernel, so the host builds frame
+    // i's tables while the GPU works on frame i+1, and kernels never contend.
+    JPGE_HIP(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking));
+    for (int i = 0; i < kSlots; ++i) {
         std::unique_ptr<Slot> s(new Slot());
-        JPGE_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-        for (auto& ev : s->ev) JPGE_HIP(hipEventCreate(&ev));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocDefault));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_tab, 4 * 256 * 4, hipHostMallocDefault));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_hdr, 4096, hipHostMallocDefault));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocDefault));
-        JPGE_HIP(hipMalloc((void**)&s->d_tab, 4 * 256 * 4));
+        s->stream = e->stream_;
+        for (int k = 0; k < 8; ++k)
+            JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], (k == 3 || k >= 6) ? hipEventDisableTiming : hipEventDefault));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
+        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocDefault));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
+        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
+        JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
         e->slots_.push_back(std::move(s));
     }
     out = std::move(e);
@@ -121,9 +225,11 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
 }
 
 Encoder::~Encoder() {
+    pool_.reset();  // (no jobs are pending between calls)
     hipSetDevice(device_);
-    for (auto& s : slots_) if (s && s->stream) hipStreamSynchronize(s->stream);
+    if (stream_) hipStreamSynchronize(stream_);
     slots_.clear();
+    if (stream_) hipStreamDestroy(stream_);
     hipFree(d_dbg_);
 }
 
@@ -210,7 +316,6 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         s.out_cap = s.cap_out;
     }
     const CtlLayout L(entropy_tiles(g));
-    JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, L.total, s.stream));
 
     FdctArgs a;
     a.rgb = s.in_dev;
@@ -222,6 +327,8 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         a.q[64 + i] = (double)qc[i];
     }
     a.coef = s.d_coef;
+    a.zero = reinterpret_cast<uint32_t*>(s.d_ctl);
+    a.zero_words = (uint32_t)(L.total / 4);
     a.dbg = d_dbg_;
     StatsArgs st2;
     st2.coef = s.d_coef;
@@ -229,44 +336,55 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     st2.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
     st2.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
     st2.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
-    if (timing_) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
+    s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
+    s.tables_done.store(0, std::memory_order_relaxed);
+    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
     JPGE_HIP(launch_fdct(a, s.stream));
-    if (timing_) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
+    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
     JPGE_HIP(launch_stats(st2, s.stream));
-    if (timing_) JPGE_HIP(hipEventRecord(s.ev[2], s.stream));
-    JPGE_HIP(hipMemcpyAsync(s.h_hist->cnt, s.d_ctl + L.cnt, sizeof(s.h_hist->cnt), hipMemcpyDeviceToHost, s.stream));
-    JPGE_HIP(hipMemcpyAsync(s.h_hist->key, s.d_ctl + L.key, sizeof(s.h_hist->key), hipMemcpyDeviceToHost, s.stream));
-    JPGE_HIP(hipEventRecord(s.ev[3], s.stream));
+    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[2], s.stream));
+    s.seq = ++seq_counter_;
+    JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
+                                s.stream));
     return kOk;
 }
 
-// Phase 2: wait for the histograms, build the four tables on the host
-// (generateHuffmanCode semantics), write the headers, launch the entropy kernel.
-int Encoder::phase2(Slot& s, const FrameDesc& f, uint32_t flags) {
-    (void)flags;
-    JPGE_HIP(hipEventSynchronize(s.ev[3]));
+// Phase 2a (host; the calling thread or a pool worker): wait for the histograms,
+// build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
+// headers into the slot's pinned staging buffer.
+int Encoder::build_tables(Slot& s, bool parallel) {
+    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, /*nap=*/!parallel)) return w;
     HuffTable tabs[4];
+    int bad = 0;
+    // the four tables are independent; the AC tables dominate
+#pragma omp parallel for num_threads(4) schedule(static, 1) reduction(| : bad) if (parallel)
     for (int t = 0; t < 4; ++t) {
         uint32_t cnt[256];
         uint64_t first[256];
         for (int i = 0; i < 256; ++i) {
-            uint64_t c = 0;
-            for (int r = 0; r < kHistReplicas; ++r) c += s.h_hist->cnt[(r * 4 + t) * 256 + i];
-            cnt[i] = (uint32_t)c;
+            cnt[i] = s.h_hist->cnt[t * 256 + i];
             first[i] = ~s.h_hist->key[t * 256 + i];
         }
-        if (!build_table(cnt, first, tabs[t])) return kErrInternal;
+        if (!build_table(cnt, first, tabs[t])) {
+            bad |= 1;
+            continue;
+        }
         for (int i = 0; i < 256; ++i)
             s.h_tab[t * 256 + i] = ((uint32_t)tabs[t].len[i] << 16) | (tabs[t].code[i] & 0xFFFF);
     }
+    if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
-    const std::vector<uint8_t> hdr = jfif_headers(f.width, f.height, s.qy, s.qc, tp);
-    if (hdr.size() > 4096) return kErrInternal;
-    std::memcpy(s.h_hdr, hdr.data(), hdr.size());
+    const std::vector<uint8_t> hdr = jfif_headers(s.g.width, s.g.height, s.qy, s.qc, tp);
+    if (hdr.size() > kHdrMax) return kErrInternal;
+    std::memcpy(reinterpret_cast<uint8_t*>(s.h_tab) + kTabBytes, hdr.data(), hdr.size());
     s.hdr_len = hdr.size();
     if (s.out_cap < s.hdr_len + 2) return kErrNoSpace;
-    JPGE_HIP(hipMemcpyAsync(s.d_tab, s.h_tab, 4 * 256 * 4, hipMemcpyHostToDevice, s.stream));
-    JPGE_HIP(hipMemcpyAsync(s.out_dev, s.h_hdr, s.hdr_len, hipMemcpyHostToDevice, s.stream));
+    return kOk;
+}
+
+// Phase 2b (GPU): upload tables + headers, launch the entropy kernel.
+int Encoder::launch_entropy_phase(Slot& s) {
+    JPGE_HIP(hipMemcpyAsync(s.d_tab, s.h_tab, kTabBytes + s.hdr_len, hipMemcpyHostToDevice, s.stream));
 
     const CtlLayout L(entropy_tiles(s.g));
     EntropyArgs e;
@@ -280,20 +398,23 @@ int Encoder::phase2(Slot& s, const FrameDesc& f, uint32_t flags) {
     e.lb_bits = reinterpret_cast<uint64_t*>(s.d_ctl + L.lb_bits);
     e.lb_ff = reinterpret_cast<uint64_t*>(s.d_ctl + L.lb_ff);
     e.tails = reinterpret_cast<uint32_t*>(s.d_ctl + L.tails);
-    e.result = reinterpret_cast<uint64_t*>(s.d_ctl + L.result);
+    e.host_result = s.d_result_host;
+    e.seq = s.seq;
+    s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1)
     e.ubuf = s.d_ubuf;
     e.wgs = entropy_wgs_;
+    e.diag = diag_;
     e.dbg = d_dbg_ ? d_dbg_ + 2 * 65536 * kStampSlots : nullptr;
-    if (timing_) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
+    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
     JPGE_HIP(launch_entropy(e, s.stream));
-    if (timing_) JPGE_HIP(hipEventRecord(s.ev[5], s.stream));
-    JPGE_HIP(hipMemcpyAsync(s.h_result, s.d_ctl + L.result, 16, hipMemcpyDeviceToHost, s.stream));
+    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[5], s.stream));
     return kOk;
 }
 
 int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
-    JPGE_HIP(hipStreamSynchronize(s.stream));
-    if (timing_) {
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream)) return w;
+    if (s.timed) {
+        JPGE_HIP(wait_event(s.ev[5]));
         hipEventElapsedTime(&times_.fdct, s.ev[0], s.ev[1]);
         hipEventElapsedTime(&times_.dc_stats, s.ev[1], s.ev[2]);
         hipEventElapsedTime(&times_.entropy, s.ev[4], s.ev[5]);
@@ -303,8 +424,9 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
         times_.entropy_sum += times_.entropy;
         times_.frames += 1;
     }
+    if (stamps_file_) hipStreamSynchronize(s.stream);
     dump_stamps(s);
-    const uint64_t err = s.h_result[1];
+    const uint64_t err = s.h_result[1] | s.h_result[2];
     if (err & 4) { f.len = 0; return kErrNoSpace; }
     if (err) return kErrTimeout;
     const size_t len = (size_t)s.h_result[0];
@@ -312,7 +434,8 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
     if (flags & kFlagDeviceOutput) return kOk;
     if (len > f.cap) return kErrNoSpace;
     JPGE_HIP(hipMemcpyAsync(f.out, s.out_dev, len, hipMemcpyDeviceToHost, s.stream));
-    JPGE_HIP(hipStreamSynchronize(s.stream));
+    JPGE_HIP(hipEventRecord(s.ev[7], s.stream));
+    JPGE_HIP(wait_event(s.ev[7]));
     return kOk;
 }
 
@@ -320,9 +443,10 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *slots_[0];
     int st = phase1(s, f, qy, qc, flags);
-    if (!st) st = phase2(s, f, flags);
+    if (!st) st = build_tables(s, true);
+    if (!st) st = launch_entropy_phase(s);
     if (!st) st = finish(s, f, flags);
-    else hipStreamSynchronize(s.stream);
+    hipStreamSynchronize(s.stream);  // every output byte is in place
     f.status = st;
     return st;
 }
@@ -336,16 +460,45 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
         if (st && !first_err) first_err = st;
     };
     for (int i = 0; i < n; ++i) fr[i].status = 0;
-    // software pipeline: phase1(i) || host tables of (i-1) || drain (i-2)
-    for (int i = 0; i < n + 2; ++i) {
-        if (i < n) note(i, phase1(*slots_[i % S], fr[i], qy, qc, flags));
-        if (i - 1 >= 0 && i - 1 < n && !fr[i - 1].status) note(i - 1, phase2(*slots_[(i - 1) % S], fr[i - 1], flags));
-        if (i - 2 >= 0 && i - 2 < n) {
-            Slot& s = *slots_[(i - 2) % S];
-            if (!fr[i - 2].status) note(i - 2, finish(s, fr[i - 2], flags));
+    // Software pipeline on one stream: queue frame i's transform + statistics and
+    // hand its table build to a worker; then queue frame i-L's table upload and
+    // entropy kernel behind the L frames already queued (the host builds while the
+    // GPU works through them), and drain frame i-L-D (D iterations after its entropy
+    // launch, so the GPU keeps about D frames of queued work while the host waits).
+    if (!pool_ && n > 1) pool_.reset(new TablePool(kTableThreads));
+    const int L = kLookahead;
+    for (int i = 0; i < n + L + kDrainLag; ++i) {
+        if (i < n) {
+            Slot& s = *slots_[i % S];
+            note(i, phase1(s, fr[i], qy, qc, flags));
+            if (!fr[i].status) {
+                if (pool_) {
+                    Slot* sp = &s;
+                    const int dev = device_;
+                    pool_->submit([this, sp, dev] {
+                        hipSetDevice(dev);
+                        sp->tables_status = build_tables(*sp, false);
+                        sp->tables_done.store(1, std::memory_order_release);
+                    });
+                } else {
+                    s.tables_status = build_tables(s, true);
+                    s.tables_done.store(1, std::memory_order_release);
+                }
+            }
+        }
+        const int j = i - L, k = i - L - kDrainLag;
+        if (j >= 0 && j < n && !fr[j].status) {
+            Slot& s = *slots_[j % S];
+            while (!s.tables_done.load(std::memory_order_acquire)) std::this_thread::yield();
+            note(j, s.tables_status ? s.tables_status : launch_entropy_phase(s));
+        }
+        if (k >= 0 && k < n) {
+            Slot& s = *slots_[k % S];
+            if (!fr[k].status) note(k, finish(s, fr[k], flags));
             else hipStreamSynchronize(s.stream);
         }
     }
+    JPGE_HIP(hipStreamSynchronize(stream_));  // every output byte is in place
     return first_err;
 }
 
@@ -379,12 +532,11 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
     Slot& s = *slots_[0];
     int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput);
     if (st) { hipStreamSynchronize(s.stream); return st; }
-    JPGE_HIP(hipEventSynchronize(s.ev[3]));
+    JPGE_HIP(hipStreamSynchronize(s.stream));
     for (int t = 0; t < 4; ++t)
         for (int i = 0; i < 256; ++i) {
-            uint64_t c = 0;
-            for (int r = 0; r < kHistReplicas; ++r) c += s.h_hist->cnt[(r * 4 + t) * 256 + i];
-            counts[t * 256 + i] = (uint32_t)c;
+            const uint32_t c = s.h_hist->cnt[t * 256 + i];
+            counts[t * 256 + i] = c;
             first[t * 256 + i] = c ? ~s.h_hist->key[t * 256 + i] : ~0ull;
         }
     return kOk;

@@ -1,5 +1,5 @@
 // Host orchestration of the GPU encode path: one Encoder = one HIP device, a
-// small ring of frame slots (each with its own stream and workspace), and the
+// small ring of frame slots (each with its own workspace, all on one stream), and the
 // per-image Huffman-table build between the statistics kernels and the entropy
 // kernel.  This is the engine behind the C ABI (include/jpge.h).
 #pragma once
@@ -52,7 +52,9 @@ class Encoder {
     int symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                      uint32_t counts[1024], uint64_t first[1024]);
 
-    void set_timing(bool on) { timing_ = on; }
+    // Kernel timing with HIP events: 0 off, N >= 1 brackets the kernels of every
+    // N-th frame (events cost GPU time; sampling keeps the pipeline's shape).
+    void set_timing(int every) { timing_every_ = every > 0 ? every : 0; }
     void reset_timing() { times_ = KernelTimes(); }
     const KernelTimes& times() const { return times_; }
     int device() const { return device_; }
@@ -60,15 +62,25 @@ class Encoder {
 
   private:
     struct Slot;
+    class TablePool;
     Encoder() = default;
     int ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap);
+    // phase 1 (GPU): upload, transform + statistics kernels, histogram download
     int phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
-    int phase2(Slot& s, const FrameDesc& f, uint32_t flags);
+    // phase 2a (host, any thread): Huffman tables + headers from the histograms
+    int build_tables(Slot& s, bool parallel);
+    // phase 2b (GPU): table upload + entropy kernel
+    int launch_entropy_phase(Slot& s);
     int finish(Slot& s, FrameDesc& f, uint32_t flags);
 
     int device_ = 0;
-    bool timing_ = false;
+    hipStream_t stream_ = nullptr;
+    int timing_every_ = 0;
+    uint64_t frame_counter_ = 0;
+    uint64_t seq_counter_ = 0;
+    std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
+    uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
     uint64_t* d_dbg_ = nullptr;
     size_t dbg_words_ = 0;

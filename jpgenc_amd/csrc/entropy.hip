@@ -36,11 +36,17 @@ constexpr int kLbDepth = 4;                                           // 256 rec
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
 constexpr int kChunk = kK3Threads * kWin;                             // output bytes per round (pre-stuffing)
+// One part's bits: DC <= 16+11, 16 AC symbols <= 16+11 each, <= 3 ZRL (a part
+// spans 16 positions, so only its first run can reach 16), EOB <= 16 -> < 512.
+constexpr int kSlotWords = 16;
 
 struct K3Lds {
-    int16_t zz[kK3Blocks * kZzStride];  // staged tile; phase C: stuffed-output buffer
-    uint32_t stage[kStageWords];        // big-endian bit stage of one tile (all zero between tiles)
-    uint32_t tab[4 * 256];              // (len << 16) | code
+    union {
+        int16_t zz[kK3Blocks * kZzStride];  // staged tile (coding pass)
+        uint32_t stage[kStageWords];        // the tile's big-endian bit stream (compaction, store)
+    } u;
+    uint32_t slot[kSlotWords * kK3Threads];  // every lane's part, MSB first; word k at [k][tid]
+    uint32_t tab[4 * 256];                   // (len << 16) | code
     uint64_t bmask[kK3Blocks];
     int prevdc[6];
     uint32_t sbits[kK3Threads];  // bits of every part, stream order; then their offsets
@@ -48,33 +54,34 @@ struct K3Lds {
     uint32_t cnt8[8];
     uint32_t wg, carry, split, fill, ftotal;
     uint64_t prefix, ffprefix;
+    uint64_t err;  // this workgroup's wait timeouts (1 look-back, 2 tail)
 };
-// phase C stuffs into zz and stage, which are contiguous
-static_assert(offsetof(K3Lds, stage) == sizeof(int16_t) * kK3Blocks * kZzStride, "zz, stage contiguous");
+// phase C stuffs into u and slot, which are contiguous
+static_assert(offsetof(K3Lds, slot) == sizeof(K3Lds::u), "u, slot contiguous");
 static_assert(offsetof(K3Lds, tab) >= 2 * kChunk + 8, "stuffing buffer too small");
 static_assert((uint64_t)kMaxTiles * kK3Blocks * kStageBytesPerBlock + 8 <= kEntropyRegionBytes, "region");
 
-// MSB-first bit sink over big-endian 32-bit LDS words; a lane's first and last
-// words may be shared with its neighbours, so every word is OR-ed in.
-struct BitSink {
-    uint32_t* st;
-    uint32_t word;
-    int fill;      // bits placed in the current word (leading bits belong to others)
-    uint64_t acc;  // right-aligned pending bits of the current word
-    __device__ __forceinline__ void init(uint32_t* s, uint32_t pos) {
-        st = s; word = pos >> 5; fill = (int)(pos & 31); acc = 0;
+// MSB-first bit sink over one lane's private LDS slot (word k at s[k * stride]).
+// Branch-free: the current word is stored on every put (a partial word is simply
+// rewritten until it completes).
+struct SlotSink {
+    uint32_t* s;
+    uint32_t k;     // index of the current word
+    uint32_t cur;   // current word, MSB-aligned
+    uint32_t fill;  // bits in cur, 0..31
+    __device__ __forceinline__ void init(uint32_t* slot) { s = slot; k = 0; cur = 0; fill = 0; }
+    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {  // 0 <= n <= 32, v < 2^n
+        const uint32_t t = fill + n;                                  // <= 63
+        const uint32_t out = cur | (uint32_t)(((uint64_t)v << 32) >> t);
+        s[k * kK3Threads] = out;
+        const bool full = t >= 32;
+        cur = full ? (uint32_t)((uint64_t)v << (64 - t)) : out;
+        fill = full ? t - 32 : t;
+        k += full ? 1u : 0u;
     }
-    __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
-        acc = (acc << n) | v;
-        fill += n;
-        if (fill >= 32) {
-            fill -= 32;
-            atomicOr(&st[word++], (uint32_t)(acc >> fill));
-            acc &= (1ull << fill) - 1;
-        }
-    }
-    __device__ __forceinline__ void flush() {
-        if (fill > 0) atomicOr(&st[word], (uint32_t)(acc << (32 - fill)));
+    __device__ __forceinline__ uint32_t finish() {  // total bits
+        if (fill) s[k * kK3Threads] = cur;           // spill bits of a word-completing last put
+        return 32 * k + fill;
     }
 };
 
@@ -109,43 +116,37 @@ __device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int
     c.tdc = &L.tab[(k < 4 ? 0 : 2) * 256];
     c.tac = &L.tab[(k < 4 ? 1 : 3) * 256];
     c.mask = c.active ? L.bmask[blk] : 0ull;
-    c.pv.load(L.zz, c.mask, blk, part, c.active);
+    c.pv.load(L.u.zz, c.mask, blk, part, c.active);
     // DC difference to the chain predecessor, Image.cpp:638-678
-    c.dcdiff = (c.active && part == 0) ? L.zz[blk * kZzStride] - pred_dc(b0, blk, L.zz, L.prevdc) : 0;
+    c.dcdiff = (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc) : 0;
     return c;
 }
 
-// Bits of the part, counted (pass 1) or emitted (pass 2) in stream order.
-template <bool kEmit>
-__device__ __forceinline__ uint32_t part_bits(const PartCoder& c, BitSink* bs) {
-    uint32_t nbits = 0;
+// Emit the part into the lane's slot in stream order; returns its bit count.
+__device__ __forceinline__ uint32_t code_part(const PartCoder& c, SlotSink& bs) {
     if (c.active && c.part == 0) {
         const int dcat = category(c.dcdiff);
         const uint32_t ent = c.tdc[dcat];
-        nbits += (ent >> 16) + dcat;
-        if (kEmit) {
-            const uint32_t db = (uint32_t)(c.dcdiff < 0 ? c.dcdiff + (1 << dcat) - 1 : c.dcdiff) & ((1u << dcat) - 1);
-            bs->put(((ent & 0xFFFF) << dcat) | db, (int)(ent >> 16) + dcat);
-        }
+        const uint32_t db = (uint32_t)(c.dcdiff < 0 ? c.dcdiff + (1 << dcat) - 1 : c.dcdiff) & ((1u << dcat) - 1);
+        bs.put(((ent & 0xFFFF) << dcat) | db, (ent >> 16) + dcat);
     }
     const uint32_t zrl = c.tac[0xF0];
     for_each_ac(c.pv, c.part, [&](int p, int run, int v) {
-        const int cat = category(v);
-        if (kEmit) {
-            while (run >= 16) { bs->put(zrl & 0xFFFF, (int)(zrl >> 16)); run -= 16; }
-            const uint32_t ent = c.tac[(run << 4) | cat];
-            const uint32_t vb = (uint32_t)(v < 0 ? v + (1 << cat) - 1 : v) & ((1u << cat) - 1);
-            bs->put(((ent & 0xFFFF) << cat) | vb, (int)(ent >> 16) + cat);
-        } else {
-            nbits += (uint32_t)(run >> 4) * (zrl >> 16) + (c.tac[((run & 15) << 4) | cat] >> 16) + cat;
+        const uint32_t av = (uint32_t)(v < 0 ? -v : v);
+        __builtin_assume(av != 0);
+        const uint32_t cat = 32 - __builtin_clz(av);
+        if (run >= 16) {  // rare: up to 3 ZRL codes
+            for (; run >= 16; run -= 16) bs.put(zrl & 0xFFFF, zrl >> 16);
         }
+        const uint32_t ent = c.tac[(run << 4) | cat];
+        const uint32_t vb = (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1);  // v - 1 when negative
+        bs.put(((ent & 0xFFFF) << cat) | vb, (ent >> 16) + cat);
     });
     if (c.active && c.part == 3 && !(c.mask >> 63)) {  // EOB
         const uint32_t ent = c.tac[0];
-        nbits += ent >> 16;
-        if (kEmit) bs->put(ent & 0xFFFF, (int)(ent >> 16));
+        bs.put(ent & 0xFFFF, ent >> 16);
     }
-    return nbits;
+    return bs.finish();
 }
 
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_kernel(EntropyArgs a) {
@@ -158,18 +159,22 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         L.carry = 0;
         L.split = 0;
         L.fill = 0;
+        L.err = 0;
     }
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
-    for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
     __syncthreads();
     const uint32_t wg = L.wg, G = gridDim.x;
+    if (wg == 0) {  // the headers (SOI .. SOS) travel behind the tables
+        const uint8_t* hdr = reinterpret_cast<const uint8_t*>(a.tables + 1024);
+        for (uint32_t i = tid; i < a.hdr_len; i += kK3Threads) a.out[i] = hdr[i];
+    }
     const bool last = wg == G - 1;
     const uint32_t nblocks = a.g.nblocks();
     const uint32_t ntiles = (nblocks + kK3Blocks - 1) / kK3Blocks;
     const uint32_t tf = (uint32_t)((uint64_t)wg * ntiles / G);
     const int ntl = (int)((uint64_t)(wg + 1) * ntiles / G) - (int)tf;  // 1..kMaxTiles (entropy_grid)
-    uint64_t* err = a.result + 1;
+    uint64_t* err = &L.err;
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
     auto tile_nb = [&](uint32_t t) { return (int)min((uint64_t)kK3Blocks, nblocks - (uint64_t)t * kK3Blocks); };
@@ -183,43 +188,51 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     for (int lt = 0; lt < ntl; ++lt) {
         const uint64_t b0 = (uint64_t)(tf + lt) * kK3Blocks;
         const int nb = tile_nb(tf + lt);
-        __syncthreads();  // previous tile: zz readers done, stage re-zeroed, carry set
-        regs.stage(nb, L.zz, L.bmask, L.prevdc, tid);
+        __syncthreads();  // previous tile: stage stored, carry set (u is free)
+        regs.stage(nb, L.u.zz, L.bmask, L.prevdc, tid);
         if (lt + 1 < ntl) regs.load(a.coef, b0 + kK3Blocks, tile_nb(tf + lt + 1), tid);
         __syncthreads();
         JPGE_ACC(0, tq);
-        L.sbits[blk * 4 + part] = part_bits<false>(make_coder(L, b0, nb, blk, part), nullptr);
+        uint32_t n;  // bits of this lane's part
+        {
+            const PartCoder pc = make_coder(L, b0, nb, blk, part);
+            SlotSink ss;
+            ss.init(L.slot + tid);
+            n = code_part(pc, ss);
+        }
+        L.sbits[blk * 4 + part] = n;
         __syncthreads();
         JPGE_ACC(1, tq);
         uint32_t T;  // scan in stream order (thread tid takes stream index tid)
         const uint32_t ex = block_scan<kK3Waves>(L.sbits[tid], L.wsum, lane, wv, T);
         L.sbits[tid] = ex;
+        const uint32_t lead = wl & 31;
+        const uint32_t ncw = (lead + T) >> 5;  // complete words of the tile stream
+        for (uint32_t i = tid; i <= ncw; i += kK3Threads) L.u.stage[i] = 0;  // (zz is dead)
         __syncthreads();
         JPGE_ACC(2, tq);
-        const uint32_t excl = L.sbits[blk * 4 + part];
-        const uint32_t lead = wl & 31;
+        // compaction: OR the part's slot words into the stage at its stream offset
         {
-            const PartCoder pc = make_coder(L, b0, nb, blk, part);  // (re-read: fewer live registers)
-            BitSink bs;
-            bs.init(L.stage, lead + excl);
-            part_bits<true>(pc, &bs);
-            if (pc.active) bs.flush();
+            const uint32_t pos0 = lead + L.sbits[blk * 4 + part];
+            for (uint32_t k = 0; 32 * k < n; ++k) {
+                const uint32_t v = L.slot[k * kK3Threads + tid];
+                const uint32_t pos = pos0 + 32 * k, sh = pos & 31, len = min(32u, n - 32 * k);
+                atomicOr(&L.u.stage[pos >> 5], v >> sh);
+                if (sh + len > 32) atomicOr(&L.u.stage[(pos >> 5) + 1], v << (32 - sh));
+            }
         }
         __syncthreads();
         JPGE_ACC(3, tq);
-        const uint32_t ncw = (lead + T) >> 5;  // complete words
         const uint32_t wbase = wl >> 5;
         for (uint32_t w = tid; w < ncw; w += kK3Threads) {
-            uint32_t v = L.stage[w];
+            uint32_t v = L.u.stage[w];
             if (w == 0) v |= L.carry;  // partial last word of the previous tile
             R32[wbase + w] = __builtin_bswap32(v);
-            L.stage[w] = 0;
         }
         if (tid == 0) {  // (thread 0 consumed the old carry above)
-            uint32_t v = L.stage[ncw];
+            uint32_t v = L.u.stage[ncw];
             if (ncw == 0) v |= L.carry;
             L.carry = v;
-            L.stage[ncw] = 0;
         }
         wl += T;
         JPGE_ACC(4, tq);
@@ -318,14 +331,11 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     const uint32_t n_own = nc + ((last && eb) ? 1u : 0u);
     const uint64_t D0 = a.hdr_len + (P >> 3) + L.ffprefix;
     const uint64_t ntot = (uint64_t)n_own + ftotal + (last ? 2u : 0u);
-    if (D0 + ntot > a.out_cap) {
-        if (tid == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 4ull);
-        return;
-    }
-    uint8_t* ob = reinterpret_cast<uint8_t*>(L.zz);
+    const bool fits = D0 + ntot <= a.out_cap;
+    uint8_t* ob = reinterpret_cast<uint8_t*>(&L.u);  // (u and slot: contiguous, both dead here)
     const uint32_t split = L.split, fill = L.fill;
     uint64_t d = D0;
-    for (uint32_t c = 0; c < n_own; c += kChunk) {
+    for (uint32_t c = 0; fits && c < n_own; c += kChunk) {
         const uint32_t j0 = c + kWin * tid;
         const uint32_t jhi = min(j0 + kWin, n_own);
         uint32_t y[kWinWords];
@@ -381,12 +391,25 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         d += clen;
         __syncthreads();  // ob is rewritten by the next round
     }
-    if (last && tid == 0) {  // EOI, Image.cpp:1003-1005
-        a.out[d] = 0xFF;
-        a.out[d + 1] = 0xD9;
-        a.result[0] = d + 2;
+    if (last && tid == 0) {
+        uint64_t len = 0;
+        if (fits) {  // EOI, Image.cpp:1003-1005
+            a.out[d] = 0xFF;
+            a.out[d + 1] = 0xD9;
+            len = d + 2;
+        }
+        // length and no-space flag straight into mapped host memory: the last
+        // workgroup's end offset bounds every workgroup's, so it alone decides
+        // whether the output fits (no fence needed: the host reads after the kernel)
+        __hip_atomic_store(&a.host_result[0], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.host_result[1], (fits ? 0ull : 4ull) | L.err, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.host_result[3], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     JPGE_STAMP(6);
+    __syncthreads();
+    if (tid == 0 && L.err)  // (rare) a wait timed out: report it beside the result
+        __hip_atomic_store(&a.host_result[2], L.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace

@@ -95,6 +95,7 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
     __shared__ K1Lds lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     K1WaveLds& W = lds.w[wv];
+    for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
     if (tid < 128) {
         const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
         lds.q[c][o] = a.q[tid];

@@ -51,6 +51,8 @@ struct FdctArgs {
     int maxval;      // 255 -> exact integer colour path
     double q[128];   // luma then chroma quantisers, natural order
     int16_t* coef;
+    uint32_t* zero;       // the frame's control block, zeroed by this kernel (it runs first)
+    uint32_t zero_words;
     uint64_t* dbg;   // diagnostic phase stamps (JPGE_STAMPS builds), else unused
 };
 
@@ -64,8 +66,8 @@ struct StatsArgs {
 struct EntropyArgs {
     const int16_t* coef;
     Geometry g;
-    const uint32_t* tables;  // [4][256] (len << 16) | code
-    uint8_t* out;            // whole .jpg (header already at [0, hdr_len))
+    const uint32_t* tables;  // [4][256] (len << 16) | code, followed by the header bytes
+    uint8_t* out;            // whole .jpg; the kernel writes the header to [0, hdr_len)
     uint64_t hdr_len;
     uint64_t out_cap;
     uint8_t* ubuf;           // per-workgroup unstuffed regions (entropy_ubuf_bytes)
@@ -73,8 +75,12 @@ struct EntropyArgs {
     uint64_t* lb_bits;       // [entropy_tiles] zeroed (look-back records, per workgroup)
     uint64_t* lb_ff;         // [entropy_tiles] zeroed
     uint32_t* tails;         // [entropy_tiles] zeroed
-    uint64_t* result;        // [0] total .jpg bytes, [1] error bits
+    uint64_t* host_result;   // mapped pinned host memory: [0] .jpg bytes, [1] no-space (4) and
+                             // the last workgroup's wait timeouts, [2] other workgroups' wait
+                             // timeouts (1, 2; cleared by the host), [3] = seq, written last
+    uint64_t seq;            // the frame's sequence number
     uint32_t wgs;            // workgroup count override (0 = automatic; tests)
+    uint32_t diag;           // diagnostic switches (JPGE_DIAG; 0 in production)
     uint64_t* dbg;
 };
 
@@ -95,6 +101,9 @@ inline uint64_t entropy_ubuf_bytes(const Geometry& g, uint32_t wgs_override) {
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
+// [4][256] summed counts and keys into (mapped) host memory, then *host_seq = seq
+hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
+                              uint64_t seq, hipStream_t s);
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s);
 
 }  // namespace jpge

@@ -136,7 +136,33 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     JPGE_STAMP(3);
 }
 
+// Histogram export: one workgroup sums the replicas and writes the four final
+// histograms and first-occurrence keys straight into mapped host memory, then the
+// frame's sequence number (release-ordered after the data): the host polls that
+// word instead of waiting on an event.  A kernel boundary orders it after
+// stats_kernel; there is no device-to-host copy per frame.
+__global__ __launch_bounds__(1024) void hist_export_kernel(HistPtrs h, uint32_t* host_cnt, uint64_t* host_key,
+                                                           uint64_t* host_seq, uint64_t seq) {
+    const int t = threadIdx.x;  // (table, symbol) = (t >> 8, t & 255)
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < kHistReplicas; ++r) c += h.cnt[r * 1024 + t];
+    host_cnt[t] = c;
+    host_key[t] = h.key[t];
+    __syncthreads();
+    if (t == 0) {
+        __threadfence_system();
+        __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
+                              uint64_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(hist_export_kernel, dim3(1), dim3(1024), 0, s, h, host_cnt, host_key, host_seq, seq);
+    return hipGetLastError();
+}
 
 uint32_t stats_grid(const Geometry& g) {
     const uint32_t tiles = (g.nblocks() + kK2Blocks - 1) / kK2Blocks;

@@ -17,20 +17,20 @@ ap.add_argument("--height", type=int, default=2160)
 ap.add_argument("--quality", type=int, default=90)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--kind", type=int, default=0)
+ap.add_argument("--frames", type=int, default=1, help="distinct HBM-resident frames, encoded in turn")
 a = ap.parse_args()
 
 enc = J.Encoder(0)
-host = J.synth_rgb8(3, a.width, a.height, a.kind)
-dev = torch.from_numpy(host.reshape(-1)).cuda()
+devs = [torch.from_numpy(J.synth_rgb8(3 + i, a.width, a.height, a.kind).reshape(-1)).cuda() for i in range(a.frames)]
 cap = J.max_jpeg_bytes(a.width, a.height)
 out = torch.empty(cap, dtype=torch.uint8, device="cuda")
-frames = [(dev.data_ptr(), a.width, a.height, a.width * 3)]
+allframes = [[(d.data_ptr(), a.width, a.height, a.width * 3)] for d in devs]
 outs = [(out.data_ptr(), cap)]
-enc.encode_batch_dev(frames, outs, quality=a.quality)
+enc.encode_batch_dev(allframes[0], outs, quality=a.quality)
 enc.set_timing(True)
 enc.reset_timing()
-for _ in range(a.iters):
-    n = enc.encode_batch_dev(frames, outs, quality=a.quality)
+for it in range(a.iters):
+    n = enc.encode_batch_dev(allframes[it % a.frames], outs, quality=a.quality)
 t = enc.timing()
 f = max(1, t["frames"])
 print(f"{a.width}x{a.height} Q{a.quality} kind{a.kind}: {n[0]} bytes; fdct {t['fdct_sum']/f*1e3:.1f} us, "
