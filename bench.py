@@ -232,7 +232,10 @@ def main():
                 "avg_jpeg_bytes": int(total_bytes / (args.steps * F)),
             },
             "roofline": dict(kernel=dominant, **stages[dominant]),
+            # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px)
+            "roofline_dct_stage": dict(kernel="fdct_kernel", **stages["fdct_kernel"]),
             "stages": stages,
+            "kernel_events": f"HIP events around every {args.event_every}th frame's kernels on the encoder stream",
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)

@@ -53,12 +53,13 @@ typedef struct {
     int status;         /* [out] jpge_status of this frame */
 } jpge_frame;
 
-/* Per-kernel device times of the last frame (ms, HIP events on the encode stream). */
+/* Per-kernel device times of the last timed frame (ms, HIP events on the encoder's
+ * stream; see jpge_set_timing for sampling). */
 typedef struct {
-    float fdct;     /* K1: colour + 4:2:0 + FDCT + quantise + AC statistics */
-    float dc_stats; /* K2: DC difference statistics */
-    float entropy;  /* K3: RLE/category/Huffman emission + MCU interleave + stuffing */
-    float total;    /* first kernel start .. entropy end (includes the host table build) */
+    float fdct;     /* K1: colour + 4:2:0 + FDCT + quantise */
+    float dc_stats; /* K2: DC chain + RLE/category symbol histograms + first-occurrence keys */
+    float entropy;  /* K3: Huffman emission + MCU interleave + fill + stuffing */
+    float total;    /* K1 start .. K3 end of that frame (includes the queued work of other frames) */
     double fdct_sum, dc_stats_sum, entropy_sum; /* accumulated since jpge_reset_timing (ms) */
     uint64_t frames;                            /* frames accumulated */
 } jpge_timing;
@@ -90,7 +91,9 @@ int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t width, uint32_t
                      int maxval, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
                      size_t* len, uint32_t flags);
 
-/* Many independent frames, pipelined over the context's streams (configs 3/4). */
+/* Many independent frames, pipelined on the context's stream (configs 3/4): the
+ * transform of later frames is queued ahead of each frame's entropy kernel while
+ * host threads build that frame's tables. */
 int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
                       uint32_t flags);
 
