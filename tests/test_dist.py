@@ -1,0 +1,63 @@
+"""Multi-rank bench logic on CPU (gloo, world size 2): each rank encodes its own
+frames (distinct seeds, weak scaling, no data-path collective); the process group
+only provides barriers, the max-over-ranks time and the sum of pixels."""
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import bench
+
+    r, local, w, pg = bench.dist_setup(world)
+    bench.barrier(pg)
+    mx = bench.max_over_ranks(pg, float(rank + 1) * 0.5)
+    sm = bench.sum_over_ranks(pg, 1000.0)
+    seeds = [bench.frame_seed(r, i) for i in range(16)]
+    q.put((r, local, w, mx, sm, seeds))
+    pg.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_bench_reductions_and_frame_sharding():
+    mp = pytest.importorskip("torch.multiprocessing")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (r0, l0, w0, mx0, sm0, s0), (r1, l1, w1, mx1, sm1, s1) = res
+    assert (r0, r1, w0, w1, l0, l1) == (0, 1, 2, 2, 0, 1)
+    assert mx0 == mx1 == 1.0          # slowest rank's time
+    assert sm0 == sm1 == 2000.0       # whole-job pixels
+    assert not set(s0) & set(s1)      # every rank encodes its own frames
+    assert s0[0] == 3                 # rank 0 frame 0 = the config-3 seed
+
+
+def test_single_rank_needs_no_process_group():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    rank, local, world, pg = bench.dist_setup(1)
+    assert (rank, local, world, pg) == (0, 0, 1, None)
+    assert bench.max_over_ranks(pg, 2.5) == 2.5 and bench.sum_over_ranks(pg, 7.0) == 7.0
