@@ -187,100 +187,26 @@ __device__ __forceinline__ void for_each_ac(const PartView& pv, int part, F&& f)
     }
 }
 
-// ---- inter-workgroup primitives (MI355X_MICROARCH.md, "R2" granules) ----
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 22;
-
-__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    return v;
-}
-
-// Decoupled look-back.  Records are self-contained 8-byte {flag, value} granules
-// written by one relaxed agent-scope store each, so no payload fence is needed.
-// lookback_publish makes this id's aggregate visible (as early as possible);
-// lookback_resolve, run by one whole wave, inspects kDepth*64 predecessors per
-// pass (kDepth loads in flight per lane) and returns the exclusive prefix.
-__device__ __forceinline__ void lookback_publish(uint64_t* rec, uint32_t id, uint64_t agg, int lane) {
-    if (lane == 0) st_relaxed(&rec[id], (id == 0 ? kFlagIncl : kFlagAgg) | agg);
-}
-
-template <int kDepth>
-__device__ uint64_t lookback_resolve(uint64_t* rec, uint32_t id, uint64_t agg, uint64_t* err, int lane) {
-    if (id == 0) return 0;
-    uint64_t excl = 0;
-    int64_t end = id;
-    uint32_t spins = 0;
-    for (;;) {
-        uint64_t r[kDepth];
-#pragma unroll
-        for (int k = 0; k < kDepth; ++k) {  // window position 64k + lane (0 = nearest)
-            const int64_t idx = end - 1 - lane - 64 * k;
-            r[k] = idx >= 0 ? ld_relaxed(&rec[idx]) : kFlagIncl;
-        }
-        int first = 64 * kDepth;
-        bool waiting = false;
-#pragma unroll
-        for (int k = 0; k < kDepth; ++k) {
-            const uint64_t f = r[k] & ~kValMask;
-            const uint64_t incl = __ballot(f == kFlagIncl);
-            const uint64_t notready = __ballot(f == 0);
-            if (first == 64 * kDepth) {  // positions up to the nearest inclusive record must be ready
-                const int lim = incl ? __builtin_ctzll(incl) : 63;
-                if (notready & (lim >= 63 ? ~0ull : ((2ull << lim) - 1))) waiting = true;
-                if (incl) first = 64 * k + __builtin_ctzll(incl);
-            }
-        }
-        if (waiting) {
-            if (++spins > kSpinLimit) {
-                if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        uint64_t v = 0;
-#pragma unroll
-        for (int k = 0; k < kDepth; ++k) v += (64 * k + lane <= first) ? (r[k] & kValMask) : 0ull;
-        excl += wave_sum64(v);
-        if (first < 64 * kDepth) break;
-        end -= 64 * kDepth;
-    }
-    if (lane == 0) st_relaxed(&rec[id], kFlagIncl | (excl + agg));
-    return excl;
-}
-
-template <int kDepth>
-__device__ uint64_t lookback_wave(uint64_t* rec, uint32_t id, uint64_t agg, uint64_t* err, int lane) {
-    lookback_publish(rec, id, agg, lane);
-    return lookback_resolve<kDepth>(rec, id, agg, err, lane);
-}
-
-// block-wide exclusive scan of one u32 per thread (thread order)
-template <int kWaves>
-__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* wsum, int lane, int wv, uint32_t& total) {
-    uint32_t incl = v;
+// block-wide exclusive scan of one value per thread (thread order); wsum holds
+// kWaves values of T
+template <int kWaves, typename T, typename W>
+__device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total) {
+    static_assert(sizeof(W) == 4 && (sizeof(T) == 4 || sizeof(T) == 8), "scan word types");
+    T* ws = reinterpret_cast<T*>(wsum);
+    T incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d);
+        const T o = __shfl_up(incl, d);
         if (lane >= d) incl += o;
     }
     __syncthreads();
-    if (lane == 63) wsum[wv] = incl;
+    if (lane == 63) ws[wv] = incl;
     __syncthreads();
-    uint32_t base = 0;
+    T base = 0;
     total = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
-        const uint32_t s = wsum[w];
+        const T s = ws[w];
         if (w < wv) base += s;
         total += s;
     }

@@ -72,15 +72,12 @@ constexpr size_t kHdrMax = 4096;           // headers SOI .. SOS (<= 20 + 2*69 +
 
 // Control block, zeroed at the start of every frame by the first kernel (K1).
 struct CtlLayout {
-    size_t cnt, key, ticket, lb_bits, lb_ff, tails, total;
-    explicit CtlLayout(uint32_t ntiles) {
+    size_t cnt, key, rec, total;
+    explicit CtlLayout(uint32_t ntiles) {  // (entropy workgroups <= entropy tiles)
         size_t o = 0;
         cnt = o; o += align_up((size_t)kHistReplicas * 4 * 256 * 4, 256);
         key = o; o += align_up(4 * 256 * 8, 256);
-        ticket = o; o += 256;
-        lb_bits = o; o += align_up((size_t)ntiles * 8, 256);
-        lb_ff = o; o += align_up((size_t)ntiles * 8, 256);
-        tails = o; o += align_up((size_t)ntiles * 4, 256);
+        rec = o; o += align_up((size_t)ntiles * kEntropyRecordBytes, 256);
         total = o;
     }
 };
@@ -199,7 +196,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     if (e->stamps_file_) {
-        e->dbg_words_ = 3ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel
+        e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
         JPGE_HIP(hipMemset(e->d_dbg_, 0, e->dbg_words_ * 8));
     }
@@ -234,16 +231,17 @@ Encoder::~Encoder() {
 }
 
 // Diagnostic: raw per-workgroup phase stamps of the last frame, as
-// [u64 n_fdct_wg, n_stats_wg, n_entropy_wg] then 3 x 65536 x kStampSlots u64;
+// [u64 n_fdct_wg, n_stats_wg, n_code_wg, n_pack_wg] then 4 x 65536 x kStampSlots u64;
 // the buffer is cleared afterwards (slots 8-15 accumulate).
 void Encoder::dump_stamps(const Slot& s) {
     if (!stamps_file_ || !d_dbg_) return;
     std::vector<uint64_t> h(dbg_words_);
     if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const uint64_t hdr[3] = {fdct_grid(s.g), stats_grid(s.g), entropy_grid(s.g, entropy_wgs_)};
+    const uint64_t hdr[4] = {fdct_grid(s.g), stats_grid(s.g), entropy_grid(s.g, entropy_wgs_),
+                             entropy_grid(s.g, entropy_wgs_)};
     FILE* f = std::fopen(stamps_file_, "wb");
     if (!f) return;
-    std::fwrite(hdr, 8, 3, f);
+    std::fwrite(hdr, 8, 4, f);
     std::fwrite(h.data(), 8, h.size(), f);
     std::fclose(f);
     hipMemset(d_dbg_, 0, dbg_words_ * 8);
@@ -394,10 +392,7 @@ int Encoder::launch_entropy_phase(Slot& s) {
     e.out = s.out_dev;
     e.hdr_len = s.hdr_len;
     e.out_cap = s.out_cap;
-    e.ticket = reinterpret_cast<uint32_t*>(s.d_ctl + L.ticket);
-    e.lb_bits = reinterpret_cast<uint64_t*>(s.d_ctl + L.lb_bits);
-    e.lb_ff = reinterpret_cast<uint64_t*>(s.d_ctl + L.lb_ff);
-    e.tails = reinterpret_cast<uint32_t*>(s.d_ctl + L.tails);
+    e.rec = s.d_ctl + L.rec;
     e.host_result = s.d_result_host;
     e.seq = s.seq;
     s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1)

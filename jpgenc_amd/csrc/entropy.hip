@@ -1,26 +1,26 @@
-// K3 entropy_kernel (gfx950): Huffman emission (Image.cpp:737-829) in MCU
+// K3 entropy coding (gfx950): Huffman emission (Image.cpp:737-829) in MCU
 // interleave order (Image.cpp:957-968), 1-fill and 0xFF00 stuffing
-// (BitstreamGeneric.hpp:213-248), EOI (Image.cpp:1003-1005).
+// (BitstreamGeneric.hpp:213-248), EOI (Image.cpp:1003-1005).  Two launches:
 //
-// Persistent: a workgroup takes a ticket w (dynamic, so every predecessor it waits
-// for is already resident) and owns the contiguous tiles [w*T/G, (w+1)*T/G) of
-// 128 blocks (2..kEntropyMaxTilesPerWg tiles; 4 lanes per block).
-//   A   per tile (the next tile loads into registers meanwhile): stage, bit length
-//       of every lane's share, tile scan, emit at the workgroup-LOCAL bit offset
-//       into a big-endian LDS word stage, carry the partial last word to the next
-//       tile, store complete words to this workgroup's private region R.
-//       Publish the workgroup's bit total (look-back record 1).
-//   cnt count the 0xFF bytes the stream would hold at each of the 8 possible byte
-//       alignments (still before the global offset is known).
-//   L1  resolve the bit offset P; b = P & 7 is the alignment.  Publish the split
-//       last byte (tail) for workgroup w+1; take w-1's tail for the split first
-//       byte (a byte belongs to the workgroup holding its last bit); the last
-//       workgroup 1-fills its final byte.
-//   L2  look-back over the 0xFF counts -> stuffed output offset.
-//   C   copy R to the output shifted right by b bits, a 0x00 after every 0xFF,
-//       16 KB of R per round through LDS, aligned 4-byte stores.
-// Global traffic: the coefficients once (HBM), R written once and read twice
-// (L2-resident, workgroup-private lines), the output once.
+// entropy_code_kernel — G persistent workgroups; workgroup w owns the contiguous
+//   tiles [w*T/G, (w+1)*T/G) of 128 blocks (2..kEntropyMaxTilesPerWg tiles).
+//   Per tile (the next tile loads into registers meanwhile): stage, each lane
+//   emits its part (DC / 16 zig-zag positions / EOB) once into a private LDS slot,
+//   tile scan of the part lengths, compaction into a big-endian word stage at the
+//   workgroup-LOCAL bit offset, complete words to the workgroup's private region R
+//   (the partial last word carries into the next tile).  Then the workgroup counts
+//   the 0xFF bytes its stream would hold at each of the 8 byte alignments and
+//   writes a record {bits, first 8 bits, last 8 bits, ff[8]}.
+// entropy_pack_kernel — G workgroups; each scans all G records (L2-resident): bit
+//   offset P of its stream, alignment b = P & 7, the stuffed-byte prefix (every
+//   record's count at its own alignment plus the bytes split between neighbours,
+//   rebuilt from their edge bits) — then copies R shifted right by b bits to the
+//   output with a 0x00 after every 0xFF (LDS, aligned 4-byte stores).  A byte
+//   belongs to the workgroup holding its last bit; the last one 1-fills and writes
+//   EOI.  No workgroup ever waits for another: the kernel boundary is the only
+//   synchronisation.
+// Global traffic: the coefficients once (HBM); R written once, read twice (L2 /
+// Infinity Cache, workgroup-private lines); the records; the output once.
 #include "device_common.hpp"
 
 namespace jpge {
@@ -32,13 +32,22 @@ constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
 constexpr int kMaxTiles = kEntropyMaxTilesPerWg;
 constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-case tile + lead
-constexpr int kLbDepth = 4;                                           // 256 records per look-back pass
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
 constexpr int kChunk = kK3Threads * kWin;                             // output bytes per round (pre-stuffing)
 // One part's bits: DC <= 16+11, 16 AC symbols <= 16+11 each, <= 3 ZRL (a part
 // spans 16 positions, so only its first run can reach 16), EOB <= 16 -> < 512.
 constexpr int kSlotWords = 16;
+
+// per-workgroup record handed from the code kernel to the pack kernel
+struct alignas(16) WgRecord {
+    uint32_t ff[8];  // ff[b]: 0xFF bytes wholly inside the stream when it starts at bit b (mod 8)
+    uint32_t bits;   // length of the workgroup's stream
+    uint32_t edge;   // first 8 bits | last 8 bits << 8 (each as an MSB-first byte)
+    uint32_t pad[2];
+};
+constexpr int kRecBits = 8, kRecEdge = 9;  // u32 indices
+static_assert(sizeof(WgRecord) == kEntropyRecordBytes, "record size");
 
 struct K3Lds {
     union {
@@ -52,14 +61,8 @@ struct K3Lds {
     uint32_t sbits[kK3Threads];  // bits of every part, stream order; then their offsets
     uint32_t wsum[kK3Waves];
     uint32_t cnt8[8];
-    uint32_t wg, carry, split, fill, ftotal;
-    uint64_t prefix, ffprefix;
-    uint64_t err;  // this workgroup's wait timeouts (1 look-back, 2 tail)
+    uint32_t carry;
 };
-// phase C stuffs into u and slot, which are contiguous
-static_assert(offsetof(K3Lds, slot) == sizeof(K3Lds::u), "u, slot contiguous");
-static_assert(offsetof(K3Lds, tab) >= 2 * kChunk + 8, "stuffing buffer too small");
-static_assert((uint64_t)kMaxTiles * kK3Blocks * kStageBytesPerBlock + 8 <= kEntropyRegionBytes, "region");
 
 // MSB-first bit sink over one lane's private LDS slot (word k at s[k * stride]).
 // Branch-free: the current word is stored on every put (a partial word is simply
@@ -149,37 +152,31 @@ __device__ __forceinline__ uint32_t code_part(const PartCoder& c, SlotSink& bs) 
     return bs.finish();
 }
 
-__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_kernel(EntropyArgs a) {
+__device__ __forceinline__ void tile_range(const Geometry& g, uint32_t w, uint32_t G, uint32_t& tf, int& ntl) {
+    const uint32_t ntiles = (g.nblocks() + kK3Blocks - 1) / kK3Blocks;
+    tf = (uint32_t)((uint64_t)w * ntiles / G);
+    ntl = (int)((uint64_t)(w + 1) * ntiles / G) - (int)tf;  // 1..kMaxTiles (entropy_grid)
+}
+
+__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_code_kernel(
+    EntropyArgs a) {
     __shared__ K3Lds L;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int blk = block_of(wv, lane), part = part_of(wv);
+    const uint32_t wg = blockIdx.x;
     JPGE_STAMP(0);
-    if (tid == 0) {
-        L.wg = atomicAdd(a.ticket, 1u);
-        L.carry = 0;
-        L.split = 0;
-        L.fill = 0;
-        L.err = 0;
-    }
+    if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
-    __syncthreads();
-    const uint32_t wg = L.wg, G = gridDim.x;
-    if (wg == 0) {  // the headers (SOI .. SOS) travel behind the tables
-        const uint8_t* hdr = reinterpret_cast<const uint8_t*>(a.tables + 1024);
-        for (uint32_t i = tid; i < a.hdr_len; i += kK3Threads) a.out[i] = hdr[i];
-    }
-    const bool last = wg == G - 1;
     const uint32_t nblocks = a.g.nblocks();
-    const uint32_t ntiles = (nblocks + kK3Blocks - 1) / kK3Blocks;
-    const uint32_t tf = (uint32_t)((uint64_t)wg * ntiles / G);
-    const int ntl = (int)((uint64_t)(wg + 1) * ntiles / G) - (int)tf;  // 1..kMaxTiles (entropy_grid)
-    uint64_t* err = &L.err;
+    uint32_t tf;
+    int ntl;
+    tile_range(a.g, wg, gridDim.x, tf, ntl);
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
     auto tile_nb = [&](uint32_t t) { return (int)min((uint64_t)kK3Blocks, nblocks - (uint64_t)t * kK3Blocks); };
 
-    // ---- A: emit every tile at workgroup-local bit offsets into R ----
+    // ---- emit every tile at workgroup-local bit offsets into R ----
     TileRegs<kK3Threads, kK3Blocks> regs;
     regs.init(tid);
     regs.load(a.coef, (uint64_t)tf * kK3Blocks, tile_nb(tf), tid);
@@ -188,7 +185,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     for (int lt = 0; lt < ntl; ++lt) {
         const uint64_t b0 = (uint64_t)(tf + lt) * kK3Blocks;
         const int nb = tile_nb(tf + lt);
-        __syncthreads();  // previous tile: stage stored, carry set (u is free)
+        __syncthreads();  // previous tile: stage stored, carry set (u is free); tables loaded
         regs.stage(nb, L.u.zz, L.bmask, L.prevdc, tid);
         if (lt + 1 < ntl) regs.load(a.coef, b0 + kK3Blocks, tile_nb(tf + lt + 1), tid);
         __syncthreads();
@@ -237,25 +234,22 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         wl += T;
         JPGE_ACC(4, tq);
     }
-    const uint32_t Lb = wl;  // this workgroup's bits
+    const uint32_t Lb = wl;  // this workgroup's bits (>= 12: every block codes >= 2 bits)
     if (tid == 0 && (Lb & 31)) R32[Lb >> 5] = __builtin_bswap32(L.carry);
-    if (wv == 0) lookback_publish(a.lb_bits, wg, Lb, lane);
     vm_drain();
     __syncthreads();
     JPGE_STAMP(1);
 
-    // ---- cnt: 0xFF bytes of the stream at each byte alignment b ----
-    // Output byte j (b = alignment) = local stream bits [8j - b, 8j - b + 8); byte 0
-    // is split with the predecessor when b != 0, the byte after the last complete
-    // one is the tail or the 1-filled final byte: both counted at the edges below.
+    // ---- 0xFF bytes of the stream at each byte alignment b ----
+    // Starting at global bit offset P (b = P & 7), output byte j of this workgroup
+    // holds local bits [8j - b, 8j - b + 8): it is 0xFF iff 8 one-bits start at
+    // s = 8j - b.  Mark every run start (y), count the starts with s = -b (mod 8).
+    // Starts s < 0 (the byte split with the predecessor) do not exist and runs past
+    // Lb meet the zero padding, so ff[b] counts exactly the bytes wholly inside.
     const uint32_t nwr = (Lb + 31) >> 5;  // words of R
     auto rword = [&](int64_t m) -> uint32_t {  // big-endian value of R word m (0 outside)
         return (m >= 0 && m < (int64_t)nwr) ? __builtin_bswap32(R32[m]) : 0u;
     };
-    // A byte of alignment b is 0xFF iff 8 one-bits start at local bit s = 8j - b:
-    // mark every run start (y), then count the starts with s = -b (mod 8).  Starts
-    // s < 0 (the split byte) do not exist and runs past Lb meet the zero padding,
-    // so exactly the bytes [b ? 1 : 0, nc) are counted.
     {
         uint32_t c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (uint32_t m = tid; m < nwr; m += kK3Threads) {
@@ -274,66 +268,115 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
             if (lane == 0 && s) atomicAdd(&L.cnt8[b], s);
         }
     }
+    __syncthreads();
+    if (tid < 3) {
+        uint32_t* rec = reinterpret_cast<uint32_t*>(a.rec + (uint64_t)wg * kEntropyRecordBytes);
+        if (tid == 0) {
+            // first 8 bits; last 8 bits (the 16-bit window holding them is inside R)
+            const uint32_t head = R8[0];
+            const uint32_t s0 = Lb - 8, byte = s0 >> 3, sh = s0 & 7;
+            const uint32_t tail = ((((uint32_t)R8[byte] << 8) | R8[byte + 1]) >> (8 - sh)) & 0xFF;
+            *reinterpret_cast<uint4*>(rec + 8) = make_uint4(Lb, head | (tail << 8), 0u, 0u);
+        } else {
+            const int b0 = 4 * (tid - 1);  // ff[0..3], ff[4..7]
+            *reinterpret_cast<uint4*>(rec + b0) =
+                make_uint4(L.cnt8[b0], L.cnt8[b0 + 1], L.cnt8[b0 + 2], L.cnt8[b0 + 3]);
+        }
+    }
     JPGE_STAMP(2);
+}
 
-    // ---- L1: global bit offset ----
-    if (wv == 0) {
-        const uint64_t pre = lookback_resolve<kLbDepth>(a.lb_bits, wg, Lb, err, lane);
-        if (lane == 0) L.prefix = pre;
+struct PackLds {
+    uint8_t ob[2 * kChunk + 8];  // stuffed output of one round
+    uint32_t wsum[2 * kK3Waves];  // (room for 64-bit scans)
+    uint64_t P, Q;
+    uint32_t Lb, ftotal, split, fill;
+};
+
+__global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a) {
+    __shared__ PackLds S;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t wg = blockIdx.x, G = gridDim.x;
+    const bool last = wg == G - 1;
+    JPGE_STAMP(0);
+    if (wg == 0) {  // the headers (SOI .. SOS) travel behind the tables
+        const uint8_t* hdr = reinterpret_cast<const uint8_t*>(a.tables + 1024);
+        for (uint32_t i = tid; i < a.hdr_len; i += kK3Threads) a.out[i] = hdr[i];
+    }
+
+    // ---- scan of all records: this workgroup's bit offset P and 0xFF prefix Q ----
+    // Thread t takes records [t*per, (t+1)*per).  The byte split between records
+    // k-1 and k (alignment b_k = P_k & 7 != 0) is rebuilt from k-1's last b_k bits
+    // and k's first 8 - b_k bits and counted for k (its owner); the last record's
+    // 1-filled final byte is counted for it.
+    const uint32_t per = (G + kK3Threads - 1) / kK3Threads;
+    const uint32_t k0 = min(G, tid * per), k1 = min(G, k0 + per);
+    auto rec = [&](uint32_t k) { return reinterpret_cast<const uint32_t*>(a.rec + (uint64_t)k * kEntropyRecordBytes); };
+    auto split_byte = [&](uint32_t k, uint32_t b, uint32_t edge) -> uint32_t {  // b != 0, k > 0
+        const uint32_t ptail = (rec(k - 1)[kRecEdge] >> 8) & 0xFF;
+        return (((ptail & ((1u << b) - 1)) << (8 - b)) | ((edge & 0xFF) >> b)) & 0xFF;
+    };
+    auto fill_byte = [&](uint32_t eb, uint32_t edge) -> uint32_t {  // Bitstream::fill, BitstreamGeneric.hpp:243-248
+        return ((((edge >> 8) & ((1u << eb) - 1)) << (8 - eb)) | (0xFFu >> eb)) & 0xFF;
+    };
+    // 0xFF bytes owned by record k when its stream starts at global bit p
+    auto owned_ff = [&](uint32_t k, uint64_t p) -> uint32_t {
+        const uint32_t* r = rec(k);
+        const uint32_t b = (uint32_t)(p & 7), edge = r[kRecEdge];
+        uint32_t f = r[b];
+        if (b && k > 0) f += split_byte(k, b, edge) == 0xFF;
+        const uint32_t eb = (uint32_t)((p + r[kRecBits]) & 7);
+        if (k == G - 1 && eb) f += fill_byte(eb, edge) == 0xFF;
+        return f;
+    };
+    uint64_t lsum = 0;
+    for (uint32_t k = k0; k < k1; ++k) lsum += rec(k)[kRecBits];
+    uint64_t ltot;
+    const uint64_t pbase = block_scan<kK3Waves>(lsum, S.wsum, lane, wv, ltot);
+    uint64_t fsum = 0;
+    {
+        uint64_t p = pbase;
+        for (uint32_t k = k0; k < k1; ++k) {
+            fsum += owned_ff(k, p);
+            p += rec(k)[kRecBits];
+        }
+    }
+    uint64_t ftot;
+    const uint64_t fbase = block_scan<kK3Waves>(fsum, S.wsum, lane, wv, ftot);
+    if (k0 <= wg && wg < k1) {  // this workgroup's record: offsets and edge bytes
+        uint64_t p = pbase, q = fbase;
+        for (uint32_t k = k0; k < wg; ++k) {
+            q += owned_ff(k, p);
+            p += rec(k)[kRecBits];
+        }
+        const uint32_t* r = rec(wg);
+        const uint32_t b = (uint32_t)(p & 7), bits = r[kRecBits], edge = r[kRecEdge];
+        const uint32_t eb = (uint32_t)((p + bits) & 7);
+        S.P = p;
+        S.Q = q;
+        S.Lb = bits;
+        S.ftotal = owned_ff(wg, p);
+        S.split = (b && wg > 0) ? split_byte(wg, b, edge) : 0u;
+        S.fill = (last && eb) ? fill_byte(eb, edge) : 0u;
     }
     __syncthreads();
-    const uint64_t P = L.prefix;
-    const uint32_t b = (uint32_t)(P & 7);
+    JPGE_STAMP(1);
+
+    // ---- shifted, stuffed copy R -> output ----
+    const uint64_t P = S.P;
+    const uint32_t b = (uint32_t)(P & 7), Lb = S.Lb, ftotal = S.ftotal;
     const uint32_t nc = (b + Lb) >> 3;  // complete output bytes
     const uint32_t eb = (b + Lb) & 7;   // bits in the byte after them
-    JPGE_STAMP(3);
-
-    // ---- edges: tail for w+1, split first byte, 1-fill ----
-    if (tid == 0) {
-        auto rbyte = [&](int64_t j) -> uint32_t { return (j >= 0 && j < 4 * (int64_t)nwr) ? R8[j] : 0u; };
-        uint32_t extra = 0;
-        if (eb) {
-            const uint32_t t = (((rbyte((int64_t)nc - 1) << 8) | rbyte(nc)) >> b) & 0xFF;
-            if (last) {  // Bitstream::fill(), BitstreamGeneric.hpp:243-248
-                L.fill = t | (0xFFu >> eb);
-                extra += L.fill == 0xFF;
-            } else {
-                __hip_atomic_store(&a.tails[wg], 0x80000000u | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (b) {
-            uint32_t t = 0, spins = 0;
-            while (!((t = __hip_atomic_load(&a.tails[wg - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 31)) {
-                if (++spins > kSpinLimit) {
-                    atomicOr(reinterpret_cast<unsigned long long*>(err), 2ull);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            L.split = (t & 0xFF) | (rbyte(0) >> b);
-            extra += L.split == 0xFF;
-        }
-        L.ftotal = L.cnt8[b] + extra;
-    }
-    __syncthreads();
-    const uint32_t ftotal = L.ftotal;
-    JPGE_STAMP(4);
-
-    // ---- L2: stuffed-byte offset ----
-    if (wv == 0) {
-        const uint64_t pre = lookback_wave<kLbDepth>(a.lb_ff, wg, ftotal, err, lane);
-        if (lane == 0) L.ffprefix = pre;
-    }
-    __syncthreads();
-    JPGE_STAMP(5);
-
-    // ---- C: shifted, stuffed copy R -> output ----
     const uint32_t n_own = nc + ((last && eb) ? 1u : 0u);
-    const uint64_t D0 = a.hdr_len + (P >> 3) + L.ffprefix;
+    const uint64_t D0 = a.hdr_len + (P >> 3) + S.Q;
     const uint64_t ntot = (uint64_t)n_own + ftotal + (last ? 2u : 0u);
     const bool fits = D0 + ntot <= a.out_cap;
-    uint8_t* ob = reinterpret_cast<uint8_t*>(&L.u);  // (u and slot: contiguous, both dead here)
-    const uint32_t split = L.split, fill = L.fill;
+    const uint32_t split = S.split, fill = S.fill;
+    const uint32_t* R32 = reinterpret_cast<const uint32_t*>(a.ubuf + (uint64_t)wg * kEntropyRegionBytes);
+    const uint32_t nwr = (Lb + 31) >> 5;
+    auto rword = [&](int64_t m) -> uint32_t {
+        return (m >= 0 && m < (int64_t)nwr) ? __builtin_bswap32(R32[m]) : 0u;
+    };
     uint64_t d = D0;
     for (uint32_t c = 0; fits && c < n_own; c += kChunk) {
         const uint32_t j0 = c + kWin * tid;
@@ -362,7 +405,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
         uint32_t chunk_ff;
-        const uint32_t excl = block_scan<kK3Waves>(cff, L.wsum, lane, wv, chunk_ff);
+        const uint32_t excl = block_scan<kK3Waves>(cff, S.wsum, lane, wv, chunk_ff);
         const uint32_t cend = min(c + (uint32_t)kChunk, n_own);
         const uint32_t align = (uint32_t)(d & 3);
         if (j0 < jhi) {
@@ -371,8 +414,8 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
             for (int q = 0; q < kWin; ++q) {
                 if (j0 + q < jhi) {
                     const uint8_t v = (uint8_t)(y[q >> 2] >> (24 - 8 * (q & 3)));
-                    ob[o++] = v;
-                    if (v == 0xFF) ob[o++] = 0;
+                    S.ob[o++] = v;
+                    if (v == 0xFF) S.ob[o++] = 0;
                 }
             }
         }
@@ -383,9 +426,9 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         for (uint32_t w = tid; w < nw; w += kK3Threads) {
             const uint32_t s = 4 * w, e = s + 4;
             if (s >= align && e <= align + clen) {
-                *reinterpret_cast<uint32_t*>(gout + s) = *reinterpret_cast<const uint32_t*>(ob + s);
+                *reinterpret_cast<uint32_t*>(gout + s) = *reinterpret_cast<const uint32_t*>(S.ob + s);
             } else {
-                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = ob[q];
+                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = S.ob[q];
             }
         }
         d += clen;
@@ -402,21 +445,17 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         // workgroup's end offset bounds every workgroup's, so it alone decides
         // whether the output fits (no fence needed: the host reads after the kernel)
         __hip_atomic_store(&a.host_result[0], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.host_result[1], (fits ? 0ull : 4ull) | L.err, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.host_result[1], fits ? 0ull : 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.host_result[3], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    JPGE_STAMP(6);
-    __syncthreads();
-    if (tid == 0 && L.err)  // (rare) a wait timed out: report it beside the result
-        __hip_atomic_store(&a.host_result[2], L.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    JPGE_STAMP(2);
 }
 
 }  // namespace
 
 // Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size), at least two
 // each when the frame has two tiles (so a workgroup's stream holds >= 8 bits and
-// its split first byte and tail byte differ); 512 = two per CU (LDS, registers).
+// its split first byte and last byte differ); 512 = two per CU (LDS, registers).
 uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) {
     const uint32_t nt = entropy_tiles(g);
     if (nt <= 1) return 1;
@@ -426,7 +465,13 @@ uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) {
 }
 
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(entropy_kernel, dim3(entropy_grid(a.g, a.wgs)), dim3(kK3Threads), 0, s, a);
+    const uint32_t G = entropy_grid(a.g, a.wgs);
+    hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    EntropyArgs b = a;
+    b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
+    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
     return hipGetLastError();
 }
 

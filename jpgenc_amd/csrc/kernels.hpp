@@ -37,6 +37,7 @@ constexpr int kEntropyTile = 128;         // blocks per entropy tile (4 lanes ea
 constexpr int kEntropyMaxTilesPerWg = 4;  // tiles a persistent entropy workgroup may own
 constexpr int kStageBytesPerBlock = 216;  // >= worst-case 1665 bits of one block
 constexpr int kStampSlots = 16;           // diagnostic stamp words per workgroup (JPGE_STAMPS builds)
+constexpr int kEntropyRecordBytes = 48;   // per entropy workgroup: bits, edge bits, 0xFF counts
 
 // Tables: 0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC.
 struct HistPtrs {
@@ -71,13 +72,9 @@ struct EntropyArgs {
     uint64_t hdr_len;
     uint64_t out_cap;
     uint8_t* ubuf;           // per-workgroup unstuffed regions (entropy_ubuf_bytes)
-    uint32_t* ticket;        // zeroed per launch
-    uint64_t* lb_bits;       // [entropy_tiles] zeroed (look-back records, per workgroup)
-    uint64_t* lb_ff;         // [entropy_tiles] zeroed
-    uint32_t* tails;         // [entropy_tiles] zeroed
-    uint64_t* host_result;   // mapped pinned host memory: [0] .jpg bytes, [1] no-space (4) and
-                             // the last workgroup's wait timeouts, [2] other workgroups' wait
-                             // timeouts (1, 2; cleared by the host), [3] = seq, written last
+    uint8_t* rec;            // [entropy_grid][kEntropyRecordBytes] code -> pack kernel records
+    uint64_t* host_result;   // mapped pinned host memory: [0] .jpg bytes, [1] no-space (4),
+                             // [2] reserved (0), [3] = seq, written last
     uint64_t seq;            // the frame's sequence number
     uint32_t wgs;            // workgroup count override (0 = automatic; tests)
     uint32_t diag;           // diagnostic switches (JPGE_DIAG; 0 in production)

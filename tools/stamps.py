@@ -7,14 +7,16 @@ import argparse
 import numpy as np
 
 SLOTS = 16
+KERNELS = ["fdct", "stats", "entropy_code", "entropy_pack"]
 PHASES = {
     "fdct": ["start", "", "", "", "", "", "", "end"],
     "stats": ["start", "staged", "histogram", "flush", "", "", "", ""],
-    "entropy": ["start", "emit", "count8", "lookback1", "edges", "lookback2", "output", ""],
+    "entropy_code": ["start", "emit", "count8", "", "", "", "", ""],
+    "entropy_pack": ["start", "scan", "output", "", "", "", "", ""],
 }
 ACC = {
     "stats": ["stage", "count"],
-    "entropy": ["stage", "pass1", "scan", "emit", "store"],
+    "entropy_code": ["stage", "code", "scan", "compact", "store"],
 }
 
 
@@ -24,10 +26,11 @@ def main():
     ap.add_argument("--ghz", type=float, default=0.1)  # s_memrealtime: 100 MHz
     a = ap.parse_args()
     raw = np.fromfile(a.file, np.uint64)
-    n = raw[:3].astype(np.int64)
-    data = raw[3:].reshape(3, 65536, SLOTS).astype(np.int64)
+    nk = len(KERNELS)
+    n = raw[:nk].astype(np.int64)
+    data = raw[nk:].reshape(nk, 65536, SLOTS).astype(np.int64)
     us = lambda x: x / (a.ghz * 1e3)
-    for k, name in enumerate(["fdct", "stats", "entropy"]):
+    for k, name in enumerate(KERNELS):
         full = data[k, : n[k]]
         labels = PHASES[name]
         used = [i for i, l in enumerate(labels) if l]
