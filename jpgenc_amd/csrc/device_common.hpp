@@ -187,6 +187,26 @@ __device__ __forceinline__ void for_each_ac(const PartView& pv, int part, F&& f)
     }
 }
 
+// Histogram export: sum the replicas and write the four final histograms and
+// first-occurrence keys into mapped host memory, then the frame's sequence number
+// (release-ordered after the data): the host polls that word.  One workgroup.
+template <int kThreads>
+__device__ __forceinline__ void export_hist(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key,
+                                            uint64_t* host_seq, uint64_t seq, int tid) {
+    for (int t = tid; t < 1024; t += kThreads) {  // (table, symbol) = (t >> 8, t & 255)
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < kHistReplicas; ++r) c += h.cnt[r * 1024 + t];
+        host_cnt[t] = c;
+        host_key[t] = h.key[t];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence_system();
+        __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // block-wide exclusive scan of one value per thread (thread order); wsum holds
 // kWaves values of T
 template <int kWaves, typename T, typename W>

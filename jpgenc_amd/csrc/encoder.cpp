@@ -155,7 +155,8 @@ struct Encoder::Slot {
     // pinned host staging
     HostHist* h_hist = nullptr;
     HostHist* d_hist_host = nullptr;  // device view of h_hist
-    uint32_t* h_tab = nullptr;     // same layout as d_tab
+    uint32_t* h_tab = nullptr;     // same layout as d_tab (mapped)
+    uint32_t* d_tab_host = nullptr;  // device view of h_tab
     uint64_t* h_result = nullptr;  // mapped: written by the entropy kernel's last workgroup
     uint64_t* d_result_host = nullptr;
     // per-frame state between phases
@@ -166,6 +167,7 @@ struct Encoder::Slot {
     size_t hdr_len = 0;
     uint8_t qy[64], qc[64];
     bool timed = false;                // this frame's kernels are bracketed by timing events
+    HistPtrs hist{};                   // this frame's device histograms (in d_ctl)
     uint64_t seq = 0;                  // frame sequence number (handshakes via mapped memory)
     std::atomic<int> tables_done{0};   // set by build_tables (any thread)
     int tables_status = 0;
@@ -211,7 +213,8 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
             JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], (k == 3 || k >= 6) ? hipEventDisableTiming : hipEventDefault));
         JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
         JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocDefault));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
+        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_tab_host, s->h_tab, 0));
         JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
         JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
         JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
@@ -281,7 +284,8 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
 }
 
 // Phase 1: upload (if host input), statistics kernels, histogram read-back.
-int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
+int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
+                    Slot* imp, bool export_hist) {
     if (!f.rgb || f.width == 0 || f.height == 0 || f.width > 65535 || f.height > 65535) return kErrArg;
     if (f.maxval < 1 || f.maxval > 255) return kErrRange;
     const Geometry g = geometry(f.width, f.height);
@@ -321,12 +325,15 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     a.g = g;
     a.maxval = f.maxval;
     for (int i = 0; i < 64; ++i) {
-        a.q[i] = (double)qy[i];  // Image.cpp:611-636 divides by the table entry as double
-        a.q[64 + i] = (double)qc[i];
+        a.q[i] = qy[i];
+        a.q[64 + i] = qc[i];
     }
     a.coef = s.d_coef;
     a.zero = reinterpret_cast<uint32_t*>(s.d_ctl);
     a.zero_words = (uint32_t)(L.total / 4);
+    a.imp_src = imp ? reinterpret_cast<const uint4*>(imp->d_tab_host) : nullptr;
+    a.imp_dst = imp ? reinterpret_cast<uint4*>(imp->d_tab) : nullptr;
+    a.imp_n16 = imp ? (uint32_t)((kTabBytes + imp->hdr_len + 15) / 16) : 0u;
     a.dbg = d_dbg_;
     StatsArgs st2;
     st2.coef = s.d_coef;
@@ -342,8 +349,10 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     JPGE_HIP(launch_stats(st2, s.stream));
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[2], s.stream));
     s.seq = ++seq_counter_;
-    JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
-                                s.stream));
+    s.hist = st2.hist;
+    if (export_hist)
+        JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
+                                    s.stream));
     return kOk;
 }
 
@@ -380,10 +389,15 @@ int Encoder::build_tables(Slot& s, bool parallel) {
     return kOk;
 }
 
-// Phase 2b (GPU): upload tables + headers, launch the entropy kernel.
-int Encoder::launch_entropy_phase(Slot& s) {
+// Tables + headers to the device by a copy (when no transform kernel carries them).
+int Encoder::import_tables_copy(Slot& s) {
     JPGE_HIP(hipMemcpyAsync(s.d_tab, s.h_tab, kTabBytes + s.hdr_len, hipMemcpyHostToDevice, s.stream));
+    return kOk;
+}
 
+// Phase 2b (GPU): the entropy kernels (tables already on the device); `exp`: a
+// later frame whose histograms the code kernel exports on the way.
+int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
     const CtlLayout L(entropy_tiles(s.g));
     EntropyArgs e;
     e.coef = s.d_coef;
@@ -399,6 +413,11 @@ int Encoder::launch_entropy_phase(Slot& s) {
     e.ubuf = s.d_ubuf;
     e.wgs = entropy_wgs_;
     e.diag = diag_;
+    e.exp_hist = exp ? exp->hist : HistPtrs{};
+    e.exp_cnt = exp ? exp->d_hist_host->cnt : nullptr;
+    e.exp_key = exp ? exp->d_hist_host->key : nullptr;
+    e.exp_seq = exp ? &exp->d_hist_host->seq : nullptr;
+    e.exp_seqv = exp ? exp->seq : 0;
     e.dbg = d_dbg_ ? d_dbg_ + 2 * 65536 * kStampSlots : nullptr;
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
     JPGE_HIP(launch_entropy(e, s.stream));
@@ -437,9 +456,10 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
 int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *slots_[0];
-    int st = phase1(s, f, qy, qc, flags);
+    int st = phase1(s, f, qy, qc, flags, nullptr, true);
     if (!st) st = build_tables(s, true);
-    if (!st) st = launch_entropy_phase(s);
+    if (!st) st = import_tables_copy(s);
+    if (!st) st = launch_entropy_phase(s, nullptr);
     if (!st) st = finish(s, f, flags);
     hipStreamSynchronize(s.stream);  // every output byte is in place
     f.status = st;
@@ -455,37 +475,60 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
         if (st && !first_err) first_err = st;
     };
     for (int i = 0; i < n; ++i) fr[i].status = 0;
-    // Software pipeline on one stream: queue frame i's transform + statistics and
-    // hand its table build to a worker; then queue frame i-L's table upload and
-    // entropy kernel behind the L frames already queued (the host builds while the
-    // GPU works through them), and drain frame i-L-D (D iterations after its entropy
-    // launch, so the GPU keeps about D frames of queued work while the host waits).
+    // Software pipeline on one stream.  Iteration i queues
+    //   K1(i) [carrying frame j = i-L's tables + headers to the device], K2(i),
+    //   then frame j's entropy kernels [the code kernel carrying frame i's
+    //   histograms to the host for a table worker],
+    // so the host builds a frame's tables while the GPU works through the L frames
+    // queued ahead of its entropy launch; frame i-L-D is drained D iterations after
+    // that launch (about D frames of queued GPU work while the host waits).  The
+    // pipeline's edges fall back to a standalone export kernel and a table copy.
     if (!pool_ && n > 1) pool_.reset(new TablePool(kTableThreads));
     const int L = kLookahead;
-    for (int i = 0; i < n + L + kDrainLag; ++i) {
-        if (i < n) {
-            Slot& s = *slots_[i % S];
-            note(i, phase1(s, fr[i], qy, qc, flags));
-            if (!fr[i].status) {
-                if (pool_) {
-                    Slot* sp = &s;
-                    const int dev = device_;
-                    pool_->submit([this, sp, dev] {
-                        hipSetDevice(dev);
-                        sp->tables_status = build_tables(*sp, false);
-                        sp->tables_done.store(1, std::memory_order_release);
-                    });
-                } else {
-                    s.tables_status = build_tables(s, true);
-                    s.tables_done.store(1, std::memory_order_release);
-                }
-            }
+    auto submit_tables = [&](Slot& s) {
+        if (pool_) {
+            Slot* sp = &s;
+            const int dev = device_;
+            pool_->submit([this, sp, dev] {
+                hipSetDevice(dev);
+                sp->tables_status = build_tables(*sp, false);
+                sp->tables_done.store(1, std::memory_order_release);
+            });
+        } else {
+            s.tables_status = build_tables(s, true);
+            s.tables_done.store(1, std::memory_order_release);
         }
+    };
+    for (int i = 0; i < n + L + kDrainLag; ++i) {
         const int j = i - L, k = i - L - kDrainLag;
+        Slot* sj = nullptr;  // frame j, tables built, ready for its entropy kernels
         if (j >= 0 && j < n && !fr[j].status) {
             Slot& s = *slots_[j % S];
             while (!s.tables_done.load(std::memory_order_acquire)) std::this_thread::yield();
-            note(j, s.tables_status ? s.tables_status : launch_entropy_phase(s));
+            if (s.tables_status) note(j, s.tables_status);
+            else sj = &s;
+        }
+        Slot* si = nullptr;  // frame i, whose histograms still need exporting
+        bool imported = false;
+        if (i < n) {
+            Slot& s = *slots_[i % S];
+            note(i, phase1(s, fr[i], qy, qc, flags, sj, /*export_hist=*/sj == nullptr));
+            if (!fr[i].status) {
+                imported = sj != nullptr;
+                si = sj ? &s : nullptr;
+                submit_tables(s);
+            }
+        }
+        if (sj) {
+            int st = imported ? kOk : import_tables_copy(*sj);
+            if (!st) st = launch_entropy_phase(*sj, si);
+            note(j, st);
+            if (!st) si = nullptr;  // exported by frame j's code kernel
+        }
+        if (si) {  // (frame j failed: export frame i's histograms on their own)
+            Slot& s = *slots_[i % S];
+            note(i, launch_hist_export(s.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
+                                       s.stream) == hipSuccess ? kOk : kErrHip);
         }
         if (k >= 0 && k < n) {
             Slot& s = *slots_[k % S];
@@ -501,7 +544,7 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
                         int16_t* y, int16_t* cb, int16_t* cr) {
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *slots_[0];
-    int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput);
+    int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
     if (st) { hipStreamSynchronize(s.stream); return st; }
     JPGE_HIP(hipStreamSynchronize(s.stream));
     const Geometry& g = s.g;
@@ -525,7 +568,7 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
                           uint32_t counts[1024], uint64_t first[1024]) {
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *slots_[0];
-    int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput);
+    int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
     if (st) { hipStreamSynchronize(s.stream); return st; }
     JPGE_HIP(hipStreamSynchronize(s.stream));
     for (int t = 0; t < 4; ++t)

@@ -66,11 +66,14 @@ class Encoder {
     Encoder() = default;
     int ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap);
     // phase 1 (GPU): upload, transform + statistics kernels, histogram download
-    int phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
+    // (carries `imp`'s tables to the device; exports its own histograms if asked)
+    int phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags, Slot* imp,
+               bool export_hist);
     // phase 2a (host, any thread): Huffman tables + headers from the histograms
     int build_tables(Slot& s, bool parallel);
-    // phase 2b (GPU): table upload + entropy kernel
-    int launch_entropy_phase(Slot& s);
+    // phase 2b (GPU): table upload (when not carried) + entropy kernels
+    int import_tables_copy(Slot& s);
+    int launch_entropy_phase(Slot& s, Slot* exp);
     int finish(Slot& s, FrameDesc& f, uint32_t flags);
 
     int device_ = 0;

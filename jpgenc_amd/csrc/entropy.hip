@@ -165,6 +165,8 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     const int blk = block_of(wv, lane), part = part_of(wv);
     const uint32_t wg = blockIdx.x;
     JPGE_STAMP(0);
+    if (a.exp_cnt && wg == 0)  // carried: a later frame's histograms to the host
+        export_hist<kK3Threads>(a.exp_hist, a.exp_cnt, a.exp_key, a.exp_seq, a.exp_seqv, tid);
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];

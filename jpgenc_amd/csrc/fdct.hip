@@ -96,10 +96,13 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     K1WaveLds& W = lds.w[wv];
     for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
+    if (blockIdx.x == 0)  // carried: another frame's tables + headers, host -> device
+        for (uint32_t i = tid; i < a.imp_n16; i += kK1Threads) a.imp_dst[i] = a.imp_src[i];
     if (tid < 128) {
         const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
-        lds.q[c][o] = a.q[tid];
-        lds.invq[c][o] = 1.0 / a.q[tid];
+        const double q = (double)a.q[tid];  // Image.cpp:611-636 divides by the entry as double
+        lds.q[c][o] = q;
+        lds.invq[c][o] = 1.0 / q;
     }
     __syncthreads();
     JPGE_STAMP(0);

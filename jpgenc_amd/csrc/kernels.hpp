@@ -50,10 +50,15 @@ struct FdctArgs {
     uint64_t stride;
     Geometry g;
     int maxval;      // 255 -> exact integer colour path
-    double q[128];   // luma then chroma quantisers, natural order
+    uint8_t q[128];  // luma then chroma quantisers, natural order (bytes: a small kernarg block)
     int16_t* coef;
     uint32_t* zero;       // the frame's control block, zeroed by this kernel (it runs first)
     uint32_t zero_words;
+    // carried duty: import another frame's tables + headers from mapped host memory
+    // (workgroup 0; 0 units = none)
+    const uint4* imp_src;
+    uint4* imp_dst;
+    uint32_t imp_n16;
     uint64_t* dbg;   // diagnostic phase stamps (JPGE_STAMPS builds), else unused
 };
 
@@ -76,6 +81,13 @@ struct EntropyArgs {
     uint64_t* host_result;   // mapped pinned host memory: [0] .jpg bytes, [1] no-space (4),
                              // [2] reserved (0), [3] = seq, written last
     uint64_t seq;            // the frame's sequence number
+    // carried duty of the code kernel: export another frame's histograms to mapped
+    // host memory (workgroup 0; exp_cnt == nullptr: none)
+    HistPtrs exp_hist;
+    uint32_t* exp_cnt;
+    uint64_t* exp_key;
+    uint64_t* exp_seq;
+    uint64_t exp_seqv;
     uint32_t wgs;            // workgroup count override (0 = automatic; tests)
     uint32_t diag;           // diagnostic switches (JPGE_DIAG; 0 in production)
     uint64_t* dbg;

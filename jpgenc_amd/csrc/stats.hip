@@ -141,19 +141,11 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
 // frame's sequence number (release-ordered after the data): the host polls that
 // word instead of waiting on an event.  A kernel boundary orders it after
 // stats_kernel; there is no device-to-host copy per frame.
+// (Standalone form, for single frames and the pipeline's first frames; in steady
+// state another frame's entropy code kernel carries the export.)
 __global__ __launch_bounds__(1024) void hist_export_kernel(HistPtrs h, uint32_t* host_cnt, uint64_t* host_key,
                                                            uint64_t* host_seq, uint64_t seq) {
-    const int t = threadIdx.x;  // (table, symbol) = (t >> 8, t & 255)
-    uint32_t c = 0;
-#pragma unroll
-    for (int r = 0; r < kHistReplicas; ++r) c += h.cnt[r * 1024 + t];
-    host_cnt[t] = c;
-    host_key[t] = h.key[t];
-    __syncthreads();
-    if (t == 0) {
-        __threadfence_system();
-        __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    export_hist<1024>(h, host_cnt, host_key, host_seq, seq, threadIdx.x);
 }
 
 }  // namespace
