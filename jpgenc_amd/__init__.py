@@ -204,6 +204,8 @@ class Encoder:
         self._ctx = ctypes.c_void_p()
         _check(lib().jpge_open(int(device), ctypes.byref(self._ctx)), f"jpge_open({device})")
         self.device = device
+        self._qcache = {}     # quality -> (qy, qc) byte tables
+        self._desc = None     # (key, Frame array) of the last device batch
 
     def close(self) -> None:
         if self._ctx:
@@ -260,16 +262,24 @@ class Encoder:
     def encode_batch_dev(self, frames: list[tuple[int, int, int, int]], outs: list[tuple[int, int]],
                          quality: int = 50, maxval: int = 255) -> list[int]:
         """Pipelined batch on device memory: frames = [(ptr, w, h, stride)], outs = [(ptr, cap)].
-        Returns the .jpg length of each frame (bytes stay in device memory)."""
-        qy, qc = self._tables(quality, None, None)
-        arr = (Frame * len(frames))()
-        for i, ((p, w, h, s), (o, cap)) in enumerate(zip(frames, outs)):
-            arr[i].rgb, arr[i].width, arr[i].height, arr[i].stride, arr[i].maxval = p, w, h, s, maxval
-            arr[i].out, arr[i].cap = o, cap
-        st = lib().jpge_encode_batch(self._ctx, arr, len(frames), _p(qy), _p(qc),
+        Returns the .jpg length of each frame (bytes stay in device memory).
+        The quality tables and the descriptor array of a repeated batch are reused."""
+        q = self._qcache.get(quality)
+        if q is None:
+            qy, qc = self._tables(quality, None, None)
+            q = self._qcache[quality] = (qy, qc, _p(qy), _p(qc))
+        key = (tuple(frames), tuple(outs), maxval)
+        if self._desc is None or self._desc[0] != key:
+            arr = (Frame * len(frames))()
+            for i, ((p, w, h, s), (o, cap)) in enumerate(zip(frames, outs)):
+                arr[i].rgb, arr[i].width, arr[i].height, arr[i].stride, arr[i].maxval = p, w, h, s, maxval
+                arr[i].out, arr[i].cap = o, cap
+            self._desc = (key, arr)
+        arr = self._desc[1]
+        st = lib().jpge_encode_batch(self._ctx, arr, len(frames), q[2], q[3],
                                      JPGE_DEVICE_INPUT | JPGE_DEVICE_OUTPUT)
         _check(st, "encode_batch")
-        return [arr[i].len for i in range(len(frames))]
+        return [f.len for f in arr]
 
     def encode_batch(self, frames: list[np.ndarray], quality: int = 50, maxval: int = 255) -> list[bytes]:
         qy, qc = self._tables(quality, None, None)

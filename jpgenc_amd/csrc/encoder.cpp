@@ -1,6 +1,7 @@
 #include "encoder.hpp"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -46,26 +47,38 @@ inline hipError_t wait_event(hipEvent_t e) {
 // Poll a sequence word a kernel writes into mapped host memory after its data
 // (release-ordered).  `nap`: sleep ~10 us between polls (pool workers, which have
 // slack) instead of spinning (the submitting thread).  Bounded: a stream error or
-// ~20 s without progress fails.
+// ~20 s without progress fails.  The stream is queried only after 2 ms without the
+// word (then every ms): a stream query enqueues a marker behind the newest launch,
+// which costs the GPU ~6 us of idle each time.
 inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool nap = false) {
-    auto t0 = std::chrono::steady_clock::now();
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto next_query = t0 + std::chrono::milliseconds(2);
     for (uint32_t spins = 0;; ++spins) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return kOk;
         if (nap) std::this_thread::sleep_for(std::chrono::microseconds(10));
-        if ((spins & 4095) == 4095 || (nap && (spins & 63) == 63)) {
-            const hipError_t q = hipStreamQuery(stream);
-            if (q != hipSuccess && q != hipErrorNotReady) return kErrHip;
-            if (q == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) return kErrInternal;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) return kErrTimeout;
-        }
+        if (!nap && (spins & 255) != 255) continue;
+        const auto now = clk::now();
+        if (now < next_query) continue;
+        next_query = now + std::chrono::milliseconds(1);
+        const hipError_t q = hipStreamQuery(stream);
+        if (q != hipSuccess && q != hipErrorNotReady) return kErrHip;
+        if (q == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) return kErrInternal;
+        if (now - t0 > std::chrono::seconds(20)) return kErrTimeout;
     }
 }
 
-constexpr int kSlots = 6;        // frames in flight (device workspaces)
-constexpr int kLookahead = 3;    // frames whose transform is queued ahead of an entropy launch
-constexpr int kDrainLag = 2;     // iterations between an entropy launch and its drain
-constexpr int kTableThreads = 4; // host workers building Huffman tables (one frame each)
-static_assert(kSlots >= kLookahead + kDrainLag + 1, "slot reuse");
+// Pipeline depth limits (defaults in Encoder; the slots in flight = lookahead + drain lag + 1).
+constexpr int kMaxLookahead = 8;
+constexpr int kMaxDrainLag = 4;
+constexpr int kMaxTableThreads = 16;
+
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    const long x = std::strtol(v, nullptr, 10);
+    return x < lo ? lo : x > hi ? hi : (int)x;
+}
 
 constexpr size_t kTabBytes = 4 * 256 * 4;  // code tables as uploaded
 constexpr size_t kHdrMax = 4096;           // headers SOI .. SOS (<= 20 + 2*69 + 19 + 4*277 + 14)
@@ -197,6 +210,10 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
     if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
+    e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
+    e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
+    e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
+    e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -206,7 +223,9 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     // kernels are queued ahead of frame i's entropy kernel, so the host builds frame
     // i's tables while the GPU works on frame i+1, and kernels never contend.
     JPGE_HIP(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking));
-    for (int i = 0; i < kSlots; ++i) {
+    JPGE_HIP(hipEventCreateWithFlags(&e->batch_done_, hipEventDisableTiming));
+    const int nslots = e->lookahead_ + e->drain_lag_ + 1;  // a slot is reused after its drain
+    for (int i = 0; i < nslots; ++i) {
         std::unique_ptr<Slot> s(new Slot());
         s->stream = e->stream_;
         for (int k = 0; k < 8; ++k)
@@ -229,6 +248,7 @@ Encoder::~Encoder() {
     hipSetDevice(device_);
     if (stream_) hipStreamSynchronize(stream_);
     slots_.clear();
+    if (batch_done_) hipEventDestroy(batch_done_);
     if (stream_) hipStreamDestroy(stream_);
     hipFree(d_dbg_);
 }
@@ -483,8 +503,8 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     // queued ahead of its entropy launch; frame i-L-D is drained D iterations after
     // that launch (about D frames of queued GPU work while the host waits).  The
     // pipeline's edges fall back to a standalone export kernel and a table copy.
-    if (!pool_ && n > 1) pool_.reset(new TablePool(kTableThreads));
-    const int L = kLookahead;
+    if (!pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
+    const int L = lookahead_, D = drain_lag_;
     auto submit_tables = [&](Slot& s) {
         if (pool_) {
             Slot* sp = &s;
@@ -499,8 +519,17 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
             s.tables_done.store(1, std::memory_order_release);
         }
     };
-    for (int i = 0; i < n + L + kDrainLag; ++i) {
-        const int j = i - L, k = i - L - kDrainLag;
+    // diagnostic host trace: (iteration, point, us since the call)
+    std::vector<std::array<double, 3>> trace;
+    const auto t_call = std::chrono::steady_clock::now();
+    auto mark = [&](int i, int point) {
+        if (host_trace_file_)
+            trace.push_back({(double)i, (double)point,
+                             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count()});
+    };
+    for (int i = 0; i < n + L + D; ++i) {
+        const int j = i - L, k = i - L - D;
+        mark(i, 0);
         Slot* sj = nullptr;  // frame j, tables built, ready for its entropy kernels
         if (j >= 0 && j < n && !fr[j].status) {
             Slot& s = *slots_[j % S];
@@ -508,6 +537,7 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
             if (s.tables_status) note(j, s.tables_status);
             else sj = &s;
         }
+        mark(i, 1);
         Slot* si = nullptr;  // frame i, whose histograms still need exporting
         bool imported = false;
         if (i < n) {
@@ -519,12 +549,14 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
                 submit_tables(s);
             }
         }
+        mark(i, 2);
         if (sj) {
             int st = imported ? kOk : import_tables_copy(*sj);
             if (!st) st = launch_entropy_phase(*sj, si);
             note(j, st);
             if (!st) si = nullptr;  // exported by frame j's code kernel
         }
+        mark(i, 3);
         if (si) {  // (frame j failed: export frame i's histograms on their own)
             Slot& s = *slots_[i % S];
             note(i, launch_hist_export(s.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
@@ -535,8 +567,20 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
             if (!fr[k].status) note(k, finish(s, fr[k], flags));
             else hipStreamSynchronize(s.stream);
         }
+        mark(i, 4);
     }
-    JPGE_HIP(hipStreamSynchronize(stream_));  // every output byte is in place
+    // every output byte is in place: the stream's tail, awaited by spinning (a
+    // blocking stream synchronisation adds tens of us of wake-up latency)
+    JPGE_HIP(hipEventRecord(batch_done_, stream_));
+    JPGE_HIP(wait_event(batch_done_));
+    mark(n + L + D, 5);
+    if (host_trace_file_) {
+        if (FILE* f = std::fopen(host_trace_file_, "a")) {
+            for (const auto& t : trace) std::fprintf(f, "%d %d %.2f\n", (int)t[0], (int)t[1], t[2]);
+            std::fprintf(f, "-1 -1 0\n");
+            std::fclose(f);
+        }
+    }
     return first_err;
 }
 

@@ -84,6 +84,11 @@ class Encoder {
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
+    int lookahead_ = 3;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
+    int drain_lag_ = 2;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
+    int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables
+    hipEvent_t batch_done_ = nullptr;  // end of an encode_batch's stream work
+    const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
     uint64_t* d_dbg_ = nullptr;
     size_t dbg_words_ = 0;
