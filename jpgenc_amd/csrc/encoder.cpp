@@ -49,8 +49,11 @@ inline hipError_t wait_event(hipEvent_t e) {
 // slack) instead of spinning (the submitting thread).  Bounded: a stream error or
 // ~20 s without progress fails.  The stream is queried only after 2 ms without the
 // word (then every ms): a stream query enqueues a marker behind the newest launch,
-// which costs the GPU ~6 us of idle each time.
-inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool nap = false) {
+// which costs the GPU ~6 us of idle each time.  `queued`: set once the kernel that
+// writes the word is on the stream (another thread launches it); before that an
+// idle stream is no error.
+inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool nap = false,
+                    const std::atomic<int>* queued = nullptr) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto next_query = t0 + std::chrono::milliseconds(2);
@@ -63,7 +66,9 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool
         next_query = now + std::chrono::milliseconds(1);
         const hipError_t q = hipStreamQuery(stream);
         if (q != hipSuccess && q != hipErrorNotReady) return kErrHip;
-        if (q == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) return kErrInternal;
+        if (q == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq &&
+            (!queued || queued->load(std::memory_order_acquire)))
+            return kErrInternal;
         if (now - t0 > std::chrono::seconds(20)) return kErrTimeout;
     }
 }
@@ -72,6 +77,7 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool
 constexpr int kMaxLookahead = 8;
 constexpr int kMaxDrainLag = 4;
 constexpr int kMaxTableThreads = 16;
+constexpr int kMaxLanes = 4;
 
 int env_int(const char* name, int dflt, int lo, int hi) {
     const char* v = std::getenv(name);
@@ -183,6 +189,7 @@ struct Encoder::Slot {
     HistPtrs hist{};                   // this frame's device histograms (in d_ctl)
     uint64_t seq = 0;                  // frame sequence number (handshakes via mapped memory)
     std::atomic<int> tables_done{0};   // set by build_tables (any thread)
+    std::atomic<int> export_queued{0}; // the kernel exporting this frame's histograms is launched
     int tables_status = 0;
 
     ~Slot() {
@@ -190,6 +197,63 @@ struct Encoder::Slot {
         hipFree(d_out); hipFree(d_tab);
         hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_result);
         for (auto& e : ev) if (e) hipEventDestroy(e);
+    }
+};
+
+// An independent pipeline: its own stream and slot ring; lanes other than 0 own a
+// host thread that runs the lane's share of a batch.  Between batches the thread
+// polls for ~1 ms (back-to-back batches start without a wake-up), then blocks.
+struct Encoder::Lane {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // end of the lane's batch work on its stream
+    std::vector<std::unique_ptr<Slot>> slots;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<int()> job;
+    int result = 0;
+    std::atomic<uint32_t> posted{0}, finished{0};
+    std::atomic<bool> stop{false};
+
+    void start() {
+        th = std::thread([this] {
+            prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+            uint32_t seen = 0;
+            for (;;) {
+                const auto t0 = std::chrono::steady_clock::now();
+                while (posted.load(std::memory_order_acquire) == seen && !stop.load(std::memory_order_acquire)) {
+                    if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(1)) {
+                        std::this_thread::yield();
+                        continue;
+                    }
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return posted.load(std::memory_order_acquire) != seen || stop.load(); });
+                }
+                if (posted.load(std::memory_order_acquire) == seen) return;  // stopped
+                seen = posted.load(std::memory_order_acquire);
+                result = job();
+                finished.store(seen, std::memory_order_release);
+            }
+        });
+    }
+    void post(std::function<int()> f) {
+        job = std::move(f);
+        posted.fetch_add(1, std::memory_order_acq_rel);
+        { std::lock_guard<std::mutex> g(mu); }
+        cv.notify_one();
+    }
+    int wait() {
+        const uint32_t want = posted.load(std::memory_order_acquire);
+        while (finished.load(std::memory_order_acquire) != want) std::this_thread::yield();
+        return result;
+    }
+    void shutdown() {
+        if (!th.joinable()) return;
+        stop.store(true, std::memory_order_release);
+        { std::lock_guard<std::mutex> g(mu); }
+        cv.notify_one();
+        th.join();
     }
 };
 
@@ -214,42 +278,54 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
+    e->nap_ = env_int("JPGE_NAP", 0, 0, 1) != 0;
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
         JPGE_HIP(hipMemset(e->d_dbg_, 0, e->dbg_words_ * 8));
     }
-    // One in-order stream for every slot: frame i+1's transform and statistics
-    // kernels are queued ahead of frame i's entropy kernel, so the host builds frame
-    // i's tables while the GPU works on frame i+1, and kernels never contend.
-    JPGE_HIP(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking));
-    JPGE_HIP(hipEventCreateWithFlags(&e->batch_done_, hipEventDisableTiming));
+    // Lanes: each an in-order stream whose frame i+1.. transform and statistics
+    // kernels are queued ahead of frame i's entropy kernels, so the host builds frame
+    // i's tables while the GPU works on later frames.  Two lanes interleave frames so
+    // one lane's kernels fill the other's launch tails and latency-bound phases.
+    const int nlanes = e->stamps_file_ ? 1 : env_int("JPGE_LANES", 2, 1, kMaxLanes);
     const int nslots = e->lookahead_ + e->drain_lag_ + 1;  // a slot is reused after its drain
-    for (int i = 0; i < nslots; ++i) {
-        std::unique_ptr<Slot> s(new Slot());
-        s->stream = e->stream_;
-        for (int k = 0; k < 8; ++k)
-            JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], (k == 3 || k >= 6) ? hipEventDisableTiming : hipEventDefault));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
-        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
-        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_tab_host, s->h_tab, 0));
-        JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
-        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
-        JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
-        e->slots_.push_back(std::move(s));
+    for (int l = 0; l < nlanes; ++l) {
+        std::unique_ptr<Lane> ln(new Lane());
+        ln->id = l;
+        JPGE_HIP(hipStreamCreateWithFlags(&ln->stream, hipStreamNonBlocking));
+        JPGE_HIP(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
+        for (int i = 0; i < nslots; ++i) {
+            std::unique_ptr<Slot> s(new Slot());
+            s->stream = ln->stream;
+            for (int k = 0; k < 8; ++k)
+                JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], (k == 3 || k >= 6) ? hipEventDisableTiming : hipEventDefault));
+            JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
+            JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
+            JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
+            JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_tab_host, s->h_tab, 0));
+            JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
+            JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
+            JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
+            ln->slots.push_back(std::move(s));
+        }
+        if (l > 0) ln->start();
+        e->lanes_.push_back(std::move(ln));
     }
     out = std::move(e);
     return kOk;
 }
 
 Encoder::~Encoder() {
+    for (auto& ln : lanes_) ln->shutdown();
     pool_.reset();  // (no jobs are pending between calls)
     hipSetDevice(device_);
-    if (stream_) hipStreamSynchronize(stream_);
-    slots_.clear();
-    if (batch_done_) hipEventDestroy(batch_done_);
-    if (stream_) hipStreamDestroy(stream_);
+    for (auto& ln : lanes_) {
+        if (ln->stream) hipStreamSynchronize(ln->stream);
+        ln->slots.clear();
+        if (ln->done) hipEventDestroy(ln->done);
+        if (ln->stream) hipStreamDestroy(ln->stream);
+    }
     hipFree(d_dbg_);
 }
 
@@ -363,6 +439,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     st2.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
     s.tables_done.store(0, std::memory_order_relaxed);
+    s.export_queued.store(0, std::memory_order_relaxed);
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
     JPGE_HIP(launch_fdct(a, s.stream));
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
@@ -371,8 +448,11 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.seq = ++seq_counter_;
     s.hist = st2.hist;
     if (export_hist)
+    {
         JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
                                     s.stream));
+        s.export_queued.store(1, std::memory_order_release);
+    }
     return kOk;
 }
 
@@ -380,7 +460,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel) {
-    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, /*nap=*/!parallel)) return w;
+    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, /*nap=*/!parallel, &s.export_queued)) return w;
     HuffTable tabs[4];
     int bad = 0;
     // the four tables are independent; the AC tables dominate
@@ -446,9 +526,10 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
 }
 
 int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
-    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream)) return w;
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[5]));
+        std::lock_guard<std::mutex> g(times_mu_);
         hipEventElapsedTime(&times_.fdct, s.ev[0], s.ev[1]);
         hipEventElapsedTime(&times_.dc_stats, s.ev[1], s.ev[2]);
         hipEventElapsedTime(&times_.entropy, s.ev[4], s.ev[5]);
@@ -475,7 +556,7 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
 
 int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
     JPGE_HIP(hipSetDevice(device_));
-    Slot& s = *slots_[0];
+    Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags, nullptr, true);
     if (!st) st = build_tables(s, true);
     if (!st) st = import_tables_copy(s);
@@ -488,14 +569,42 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
 
 int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
     JPGE_HIP(hipSetDevice(device_));
-    const int S = (int)slots_.size();
+    for (int i = 0; i < n; ++i) fr[i].status = 0;
+    if (n <= 0) return kOk;
+    if (!pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
+    // frames dealt round-robin to the lanes; lane 0 runs on the calling thread
+    const int nl = std::min<int>((int)lanes_.size(), n);
+    std::vector<std::vector<int>> idx(nl);
+    for (int i = 0; i < n; ++i) idx[i % nl].push_back(i);
+    for (int l = 1; l < nl; ++l)
+        lanes_[l]->post([this, l, fr, &idx, qy, qc, flags] {
+            hipSetDevice(device_);
+            return run_lane(*lanes_[l], fr, idx[l].data(), (int)idx[l].size(), qy, qc, flags);
+        });
+    // (napping on the calling thread: ~1 us timer slack for the call, restored after)
+    const long slack = nap_ ? prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0) : -1;
+    if (slack > 0) prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+    int st = run_lane(*lanes_[0], fr, idx[0].data(), (int)idx[0].size(), qy, qc, flags);
+    if (slack > 0) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+    for (int l = 1; l < nl; ++l) {
+        const int e = lanes_[l]->wait();
+        if (!st) st = e;
+    }
+    for (int i = 0; i < n; ++i)  // the first failing frame's status
+        if (fr[i].status) return fr[i].status;
+    return st;
+}
+
+int Encoder::run_lane(Lane& ln, FrameDesc* frames, const int* idx, int n, const uint8_t qy[64],
+                      const uint8_t qc[64], uint32_t flags) {
+    const int S = (int)ln.slots.size();
+    auto frame = [&](int t) -> FrameDesc& { return frames[idx[t]]; };
     int first_err = kOk;
-    auto note = [&](int i, int st) {
-        if (st && !fr[i].status) fr[i].status = st;
+    auto note = [&](int t, int st) {
+        if (st && !frame(t).status) frame(t).status = st;
         if (st && !first_err) first_err = st;
     };
-    for (int i = 0; i < n; ++i) fr[i].status = 0;
-    // Software pipeline on one stream.  Iteration i queues
+    // Software pipeline on the lane's stream (frame numbers are lane-local).  Iteration i queues
     //   K1(i) [carrying frame j = i-L's tables + headers to the device], K2(i),
     //   then frame j's entropy kernels [the code kernel carrying frame i's
     //   histograms to the host for a table worker],
@@ -503,7 +612,6 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     // queued ahead of its entropy launch; frame i-L-D is drained D iterations after
     // that launch (about D frames of queued GPU work while the host waits).  The
     // pipeline's edges fall back to a standalone export kernel and a table copy.
-    if (!pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
     const int L = lookahead_, D = drain_lag_;
     auto submit_tables = [&](Slot& s) {
         if (pool_) {
@@ -531,9 +639,12 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
         const int j = i - L, k = i - L - D;
         mark(i, 0);
         Slot* sj = nullptr;  // frame j, tables built, ready for its entropy kernels
-        if (j >= 0 && j < n && !fr[j].status) {
-            Slot& s = *slots_[j % S];
-            while (!s.tables_done.load(std::memory_order_acquire)) std::this_thread::yield();
+        if (j >= 0 && j < n && !frame(j).status) {
+            Slot& s = *ln.slots[j % S];
+            while (!s.tables_done.load(std::memory_order_acquire)) {
+                if (nap_) std::this_thread::sleep_for(std::chrono::microseconds(10));
+                else std::this_thread::yield();
+            }
             if (s.tables_status) note(j, s.tables_status);
             else sj = &s;
         }
@@ -541,9 +652,9 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
         Slot* si = nullptr;  // frame i, whose histograms still need exporting
         bool imported = false;
         if (i < n) {
-            Slot& s = *slots_[i % S];
-            note(i, phase1(s, fr[i], qy, qc, flags, sj, /*export_hist=*/sj == nullptr));
-            if (!fr[i].status) {
+            Slot& s = *ln.slots[i % S];
+            note(i, phase1(s, frame(i), qy, qc, flags, sj, /*export_hist=*/sj == nullptr));
+            if (!frame(i).status) {
                 imported = sj != nullptr;
                 si = sj ? &s : nullptr;
                 submit_tables(s);
@@ -554,30 +665,35 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
             int st = imported ? kOk : import_tables_copy(*sj);
             if (!st) st = launch_entropy_phase(*sj, si);
             note(j, st);
-            if (!st) si = nullptr;  // exported by frame j's code kernel
+            if (!st && si) {  // exported by frame j's code kernel
+                si->export_queued.store(1, std::memory_order_release);
+                si = nullptr;
+            }
         }
         mark(i, 3);
         if (si) {  // (frame j failed: export frame i's histograms on their own)
-            Slot& s = *slots_[i % S];
-            note(i, launch_hist_export(s.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
-                                       s.stream) == hipSuccess ? kOk : kErrHip);
+            const hipError_t e = launch_hist_export(si->hist, si->d_hist_host->cnt, si->d_hist_host->key,
+                                                    &si->d_hist_host->seq, si->seq, si->stream);
+            note(i, e == hipSuccess ? kOk : kErrHip);
+            if (e == hipSuccess) si->export_queued.store(1, std::memory_order_release);
         }
         if (k >= 0 && k < n) {
-            Slot& s = *slots_[k % S];
-            if (!fr[k].status) note(k, finish(s, fr[k], flags));
+            Slot& s = *ln.slots[k % S];
+            if (!frame(k).status) note(k, finish(s, frame(k), flags));
             else hipStreamSynchronize(s.stream);
         }
         mark(i, 4);
     }
     // every output byte is in place: the stream's tail, awaited by spinning (a
     // blocking stream synchronisation adds tens of us of wake-up latency)
-    JPGE_HIP(hipEventRecord(batch_done_, stream_));
-    JPGE_HIP(wait_event(batch_done_));
+    JPGE_HIP(hipEventRecord(ln.done, ln.stream));
+    JPGE_HIP(wait_event(ln.done));
     mark(n + L + D, 5);
     if (host_trace_file_) {
+        std::lock_guard<std::mutex> g(trace_mu_);
         if (FILE* f = std::fopen(host_trace_file_, "a")) {
-            for (const auto& t : trace) std::fprintf(f, "%d %d %.2f\n", (int)t[0], (int)t[1], t[2]);
-            std::fprintf(f, "-1 -1 0\n");
+            for (const auto& t : trace) std::fprintf(f, "%d %d %.2f %d\n", (int)t[0], (int)t[1], t[2], ln.id);
+            std::fprintf(f, "-1 -1 0 %d\n", ln.id);
             std::fclose(f);
         }
     }
@@ -587,7 +703,7 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
 int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                         int16_t* y, int16_t* cb, int16_t* cr) {
     JPGE_HIP(hipSetDevice(device_));
-    Slot& s = *slots_[0];
+    Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
     if (st) { hipStreamSynchronize(s.stream); return st; }
     JPGE_HIP(hipStreamSynchronize(s.stream));
@@ -611,7 +727,7 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
 int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                           uint32_t counts[1024], uint64_t first[1024]) {
     JPGE_HIP(hipSetDevice(device_));
-    Slot& s = *slots_[0];
+    Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
     if (st) { hipStreamSynchronize(s.stream); return st; }
     JPGE_HIP(hipStreamSynchronize(s.stream));

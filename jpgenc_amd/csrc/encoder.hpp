@@ -1,11 +1,14 @@
-// Host orchestration of the GPU encode path: one Encoder = one HIP device, a
-// small ring of frame slots (each with its own workspace, all on one stream), and the
-// per-image Huffman-table build between the statistics kernels and the entropy
-// kernel.  This is the engine behind the C ABI (include/jpge.h).
+// Host orchestration of the GPU encode path: one Encoder = one HIP device and a few
+// independent pipelines ("lanes"), each a stream with a small ring of frame slots
+// (each slot its own workspace), plus the per-image Huffman-table build between the
+// statistics kernels and the entropy kernels.  This is the engine behind the C ABI
+// (include/jpge.h).
 #pragma once
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -60,8 +63,11 @@ class Encoder {
     int device() const { return device_; }
     static size_t max_jpeg_bytes(uint32_t w, uint32_t h);
 
+    int lanes() const { return (int)lanes_.size(); }
+
   private:
     struct Slot;
+    struct Lane;
     class TablePool;
     Encoder() = default;
     int ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap);
@@ -75,26 +81,30 @@ class Encoder {
     int import_tables_copy(Slot& s);
     int launch_entropy_phase(Slot& s, Slot* exp);
     int finish(Slot& s, FrameDesc& f, uint32_t flags);
+    // one lane's software pipeline over frames fr[idx[0..m)]
+    int run_lane(Lane& ln, FrameDesc* fr, const int* idx, int m, const uint8_t qy[64], const uint8_t qc[64],
+                 uint32_t flags);
 
     int device_ = 0;
-    hipStream_t stream_ = nullptr;
     int timing_every_ = 0;
-    uint64_t frame_counter_ = 0;
-    uint64_t seq_counter_ = 0;
+    std::atomic<uint64_t> frame_counter_{0};
+    std::atomic<uint64_t> seq_counter_{0};
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     int lookahead_ = 3;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 2;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables
-    hipEvent_t batch_done_ = nullptr;  // end of an encode_batch's stream work
+    bool nap_ = false;          // JPGE_NAP: lane threads sleep ~10 us between polls instead of spinning
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
     uint64_t* d_dbg_ = nullptr;
     size_t dbg_words_ = 0;
     void dump_stamps(const Slot& s);
     KernelTimes times_;
-    std::vector<std::unique_ptr<Slot>> slots_;
+    std::mutex times_mu_;  // finish() of several lanes
+    std::mutex trace_mu_;
+    std::vector<std::unique_ptr<Lane>> lanes_;  // JPGE_LANES (default 2); lane 0 serves single-frame calls
 };
 
 }  // namespace jpge

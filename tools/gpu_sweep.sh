@@ -1,10 +1,7 @@
+# ad-hoc GPU sweep (used through gpurun): the bench under a few settings
 mkdir -p gpurun_out
-for cfg in a b c; do
-  r=$(timeout -k 10 200 python bench.py --no-cpu-baseline 2>>gpurun_out/sweep_err.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read().splitlines()[-1]); print(d['value'], d['ms_per_step'])") || exit 1
-  echo "$cfg $r"
+nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null
+for cfg in "2 0" "2 1" "3 0" "3 1" "4 1" "2 0" "2 1" "3 0" "3 1" "4 1"; do set -- $cfg
+  r=$(JPGE_LANES=$1 JPGE_NAP=$2 timeout -k 10 200 python bench.py --no-cpu-baseline 2>>gpurun_out/sweep_err.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read().splitlines()[-1]); print(d['value'], d['ms_per_step'])") || exit 1
+  echo "lanes=$1 nap=$2 $r"
 done
-rm -f gpurun_out/host_trace.txt
-JPGE_HOST_TRACE=gpurun_out/host_trace.txt timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 > /dev/null 2>>gpurun_out/sweep_err.log || exit 1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl9 -o tl -- python3 bench.py --no-cpu-baseline --no-kernel-events --steps 10 > /dev/null 2>&1 || exit 1
-python3 tools/timeline.py gpurun_out/tl9 --skip 400 | head -12
