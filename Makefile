@@ -12,7 +12,7 @@ LIBDIR   := jpgenc_amd/lib
 BINDIR   := jpgenc_amd/bin
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SRC) -Iinclude
-CXXFLAGS := -O2 -std=c++17 -fPIC -fopenmp -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
+CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude
 
 HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp
@@ -38,7 +38,7 @@ $(BUILD)/%.o: $(SRC)/%.cpp $(HEADERS)
 
 $(LIBDIR)/libjpge.so: $(DEV_OBJS) $(HOST_OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fopenmp -o $@ $^ -L$(ROCM)/lib -lamdhip64
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $^ -L$(ROCM)/lib -lamdhip64
 
 $(BINDIR)/jpgenc: $(SRC)/cli.cpp $(LIBDIR)/libjpge.so
 	@mkdir -p $(BINDIR)
@@ -52,7 +52,7 @@ oracle:
 # JPGE_STAMPS_FILE=<path>); never used by tests or the bench
 diag: $(DIAG_OBJS) $(HOST_OBJS)
 	@mkdir -p $(LIBDIR)/diag
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fopenmp -o $(LIBDIR)/diag/libjpge.so $^ \
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $(LIBDIR)/diag/libjpge.so $^ \
 	  -L$(ROCM)/lib -lamdhip64
 
 clean:

@@ -23,6 +23,7 @@ test-only oracle on the host cores, rank 0 at N=1.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -126,6 +127,31 @@ def cpu_baseline(args) -> dict:
     }
 
 
+def cgroup_cpu_stat() -> dict:
+    """The process cgroup's CPU accounting (usage and quota throttling), if visible."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (line.split() for line in f)}
+    except (OSError, ValueError):
+        return {}
+
+
+def thread_cpu() -> dict:
+    """CPU seconds per thread of this process, keyed (tid, name)."""
+    out = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+            name = st[st.index("(") + 1:st.rindex(")")]
+            fields = st[st.rindex(")") + 2:].split()
+            out[(tid, name)] = (int(fields[11]) + int(fields[12])) / tick
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
 def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
     """Per-launch HBM bytes per kernel from the committed rocprofv3 PMC summary."""
     try:
@@ -177,12 +203,25 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     total_bytes = 0
+    step_t = []
+    cg0 = cgroup_cpu_stat()
+    th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
     for _ in range(args.steps):
+        ts = time.perf_counter()
         lens = enc.encode_batch_dev(frames, outd, quality=args.quality)
+        step_t.append(time.perf_counter() - ts)  # (encode_batch returns with every byte in place)
         total_bytes += sum(lens)
     torch.cuda.synchronize()
     barrier(pg)
     dt = time.perf_counter() - t0
+    cg1 = cgroup_cpu_stat()
+    if th0:
+        th1 = thread_cpu()
+        use = collections.Counter()
+        for k, v in th1.items():
+            use[k] += (v - th0.get(k, 0.0)) / dt
+        print(f"threads: {len(th1)}; busiest:", {f"{k[1]}/{k[0]}": round(v, 2) for k, v in use.most_common(24)},
+              file=sys.stderr)
     tm = enc.timing()
     enc.set_timing(False)
 
@@ -235,7 +274,15 @@ def main():
             # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px)
             "roofline_dct_stage": dict(kernel="fdct_kernel", **stages["fdct_kernel"]),
             "stages": stages,
-            "kernel_events": f"HIP events around every {args.event_every}th frame's kernels on the encoder stream",
+            "kernel_events": f"HIP events around every {args.event_every}th frame's kernels on the encoder streams",
+            "step_ms": {"min": round(min(step_t) * 1e3, 3), "median": round(sorted(step_t)[len(step_t) // 2] * 1e3, 3),
+                        "max": round(max(step_t) * 1e3, 3)},
+            "lanes": enc.lanes(),
+            # host CPU use over the timed region; quota throttling stalls the pipeline
+            "host_cpu": {"cpus_used": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e6 / dt, 2),
+                         "throttled_periods": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
+                         "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3,
+                                               1)} if cg0 else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)

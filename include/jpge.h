@@ -76,6 +76,10 @@ int jpge_close(jpge_ctx* ctx);
 int jpge_set_timing(jpge_ctx* ctx, int every);
 int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t);
 int jpge_reset_timing(jpge_ctx* ctx);
+/* Pipelines ("lanes") the context runs a batch on: each lane is a HIP stream with
+ * its own frame slots and host thread; a batch's frames are dealt round-robin to
+ * them (env JPGE_LANES at jpge_open, default 4). */
+int jpge_get_lanes(jpge_ctx* ctx, int* lanes);
 
 /* Worst-case .jpg size for a frame (header + 2x worst-case entropy + EOI). */
 size_t jpge_max_jpeg_bytes(uint32_t width, uint32_t height);

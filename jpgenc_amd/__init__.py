@@ -31,7 +31,7 @@ STATUS = {
 # every symbol include/jpge.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_close", "jpge_set_timing",
-    "jpge_get_timing", "jpge_reset_timing", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
+    "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_synth_rgb8", "jpge_arai_constants",
 )
@@ -76,6 +76,7 @@ def lib() -> ctypes.CDLL:
         L.jpge_set_timing.argtypes = [vp, i32]
         L.jpge_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
         L.jpge_reset_timing.argtypes = [vp]
+        L.jpge_get_lanes.argtypes = [vp, ctypes.POINTER(i32)]
         L.jpge_device_count.argtypes = [ctypes.POINTER(i32)]
         L.jpge_max_jpeg_bytes.restype = sz
         L.jpge_max_jpeg_bytes.argtypes = [u32, u32]
@@ -241,6 +242,11 @@ class Encoder:
 
     def reset_timing(self) -> None:
         _check(lib().jpge_reset_timing(self._ctx), "reset_timing")
+
+    def lanes(self) -> int:
+        n = ctypes.c_int32()
+        _check(lib().jpge_get_lanes(self._ctx, ctypes.byref(n)), "get_lanes")
+        return n.value
 
     @staticmethod
     def _tables(quality, qy, qc):

@@ -97,6 +97,12 @@ int jpge_reset_timing(jpge_ctx* ctx) {
     return JPGE_OK;
 }
 
+int jpge_get_lanes(jpge_ctx* ctx, int* lanes) {
+    if (!ctx || !lanes) return JPGE_E_ARG;
+    *lanes = ctx->enc->lanes();
+    return JPGE_OK;
+}
+
 size_t jpge_max_jpeg_bytes(uint32_t w, uint32_t h) { return jpge::Encoder::max_jpeg_bytes(w, h); }
 
 int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]) {

@@ -1,4 +1,5 @@
 #include "encoder.hpp"
+#include "host_par.hpp"
 
 #include <algorithm>
 #include <array>
@@ -11,6 +12,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 
 #include <sys/prctl.h>
@@ -77,7 +79,11 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool
 constexpr int kMaxLookahead = 8;
 constexpr int kMaxDrainLag = 4;
 constexpr int kMaxTableThreads = 16;
-constexpr int kMaxLanes = 4;
+constexpr int kMaxLanes = 8;
+
+double abs_us(std::chrono::steady_clock::time_point t) {  // host-trace clock
+    return std::chrono::duration<double, std::micro>(t.time_since_epoch()).count();
+}
 
 int env_int(const char* name, int dflt, int lo, int hi) {
     const char* v = std::getenv(name);
@@ -110,14 +116,23 @@ struct HostHist {  // written by hist_export_kernel into mapped pinned memory
 }  // namespace
 
 // Host worker threads for the Huffman-table build (package-merge with libstdc++
-// heap order is inherently serial per table, so frames are built side by side).
+// heap order is inherently serial per table, so frames are built side by side).  A
+// job carries a readiness test (its histograms have arrived): workers take any ready
+// job, so a frame whose histograms are still queued on the GPU never holds up one
+// whose histograms are in (with several lanes, jobs finish out of order).
 class Encoder::TablePool {
   public:
+    struct Job {
+        std::function<bool()> ready;
+        std::function<void()> run;
+    };
     explicit TablePool(int n) {
         for (int i = 0; i < n; ++i)
-            th_.emplace_back([this] {
+            th_.emplace_back([this, i] {
                 prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // ~1 us sleeps while polling
-                run();
+                const std::string name = "jpge-tab" + std::to_string(i);
+                prctl(PR_SET_NAME, name.c_str(), 0, 0, 0);
+                loop();
             });
     }
     ~TablePool() {
@@ -128,7 +143,7 @@ class Encoder::TablePool {
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
-    void submit(std::function<void()> job) {
+    void submit(Job job) {
         {
             std::lock_guard<std::mutex> g(mu_);
             q_.push_back(std::move(job));
@@ -137,23 +152,32 @@ class Encoder::TablePool {
     }
 
   private:
-    void run() {
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            std::function<void()> job;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
+            if (q_.empty()) {
+                if (stop_) return;
                 cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
-                if (q_.empty()) return;
-                job = std::move(q_.front());
-                q_.pop_front();
+                continue;
             }
-            job();
+            auto it = std::find_if(q_.begin(), q_.end(), [](const Job& j) { return j.ready(); });
+            if (it == q_.end()) {  // nothing ready: nap ~10 us and look again
+                lk.unlock();
+                std::this_thread::sleep_for(std::chrono::microseconds(10));
+                lk.lock();
+                continue;
+            }
+            std::function<void()> run = std::move(it->run);
+            q_.erase(it);
+            lk.unlock();
+            run();
+            lk.lock();
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<std::function<void()>> q_;
+    std::deque<Job> q_;
     bool stop_ = false;
 };
 
@@ -190,6 +214,7 @@ struct Encoder::Slot {
     uint64_t seq = 0;                  // frame sequence number (handshakes via mapped memory)
     std::atomic<int> tables_done{0};   // set by build_tables (any thread)
     std::atomic<int> export_queued{0}; // the kernel exporting this frame's histograms is launched
+    std::chrono::steady_clock::time_point t_submit, t_start, t_done;  // table job (host trace)
     int tables_status = 0;
 
     ~Slot() {
@@ -219,6 +244,8 @@ struct Encoder::Lane {
     void start() {
         th = std::thread([this] {
             prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+            const std::string name = "jpge-lane" + std::to_string(id);
+            prctl(PR_SET_NAME, name.c_str(), 0, 0, 0);
             uint32_t seen = 0;
             for (;;) {
                 const auto t0 = std::chrono::steady_clock::now();
@@ -279,6 +306,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
     e->nap_ = env_int("JPGE_NAP", 0, 0, 1) != 0;
+    e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -286,9 +314,10 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     }
     // Lanes: each an in-order stream whose frame i+1.. transform and statistics
     // kernels are queued ahead of frame i's entropy kernels, so the host builds frame
-    // i's tables while the GPU works on later frames.  Two lanes interleave frames so
-    // one lane's kernels fill the other's launch tails and latency-bound phases.
-    const int nlanes = e->stamps_file_ ? 1 : env_int("JPGE_LANES", 2, 1, kMaxLanes);
+    // i's tables while the GPU works on later frames.  Lanes run frames side by side,
+    // so one lane's kernels fill another's launch tails and latency-bound phases
+    // (4 lanes = the hardware queues HIP opens per process; measured best).
+    const int nlanes = e->stamps_file_ ? 1 : env_int("JPGE_LANES", 4, 1, kMaxLanes);
     const int nslots = e->lookahead_ + e->drain_lag_ + 1;  // a slot is reused after its drain
     for (int l = 0; l < nlanes; ++l) {
         std::unique_ptr<Lane> ln(new Lane());
@@ -462,23 +491,21 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
 int Encoder::build_tables(Slot& s, bool parallel) {
     if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, /*nap=*/!parallel, &s.export_queued)) return w;
     HuffTable tabs[4];
-    int bad = 0;
+    int ok[4] = {0, 0, 0, 0};
     // the four tables are independent; the AC tables dominate
-#pragma omp parallel for num_threads(4) schedule(static, 1) reduction(| : bad) if (parallel)
-    for (int t = 0; t < 4; ++t) {
+    parallel_for(4, parallel ? 4 : 1, [&](long t) {
         uint32_t cnt[256];
         uint64_t first[256];
         for (int i = 0; i < 256; ++i) {
             cnt[i] = s.h_hist->cnt[t * 256 + i];
             first[i] = ~s.h_hist->key[t * 256 + i];
         }
-        if (!build_table(cnt, first, tabs[t])) {
-            bad |= 1;
-            continue;
-        }
+        if (!build_table(cnt, first, tabs[t])) return;
         for (int i = 0; i < 256; ++i)
             s.h_tab[t * 256 + i] = ((uint32_t)tabs[t].len[i] << 16) | (tabs[t].code[i] & 0xFFFF);
-    }
+        ok[t] = 1;
+    });
+    const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
     if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
     const std::vector<uint8_t> hdr = jfif_headers(s.g.width, s.g.height, s.qy, s.qc, tp);
@@ -568,37 +595,49 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
 }
 
 int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
+    const auto t_enter = std::chrono::steady_clock::now();
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
     if (!pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
-    // frames dealt round-robin to the lanes; lane 0 runs on the calling thread
+    // Frames are dealt dynamically: a lane takes the batch's next frame when its
+    // pipeline has room, so lanes finish together.  Lane 0 runs on the calling thread.
     const int nl = std::min<int>((int)lanes_.size(), n);
-    std::vector<std::vector<int>> idx(nl);
-    for (int i = 0; i < n; ++i) idx[i % nl].push_back(i);
+    std::atomic<int> next{0};
     for (int l = 1; l < nl; ++l)
-        lanes_[l]->post([this, l, fr, &idx, qy, qc, flags] {
+        lanes_[l]->post([this, l, fr, n, &next, qy, qc, flags] {
             hipSetDevice(device_);
-            return run_lane(*lanes_[l], fr, idx[l].data(), (int)idx[l].size(), qy, qc, flags);
+            return run_lane(*lanes_[l], fr, n, &next, qy, qc, flags);
         });
     // (napping on the calling thread: ~1 us timer slack for the call, restored after)
     const long slack = nap_ ? prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0) : -1;
     if (slack > 0) prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
-    int st = run_lane(*lanes_[0], fr, idx[0].data(), (int)idx[0].size(), qy, qc, flags);
+    int st = run_lane(*lanes_[0], fr, n, &next, qy, qc, flags);
     if (slack > 0) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
+    const auto t_lane0 = std::chrono::steady_clock::now();
     for (int l = 1; l < nl; ++l) {
         const int e = lanes_[l]->wait();
         if (!st) st = e;
+    }
+    if (host_trace_file_) {
+        std::lock_guard<std::mutex> g(trace_mu_);
+        if (FILE* f = std::fopen(host_trace_file_, "a")) {
+            std::fprintf(f, "-2 -2 0 -1 %.2f %.2f %.2f\n", abs_us(t_enter), abs_us(t_lane0),
+                         abs_us(std::chrono::steady_clock::now()));
+            std::fclose(f);
+        }
     }
     for (int i = 0; i < n; ++i)  // the first failing frame's status
         if (fr[i].status) return fr[i].status;
     return st;
 }
 
-int Encoder::run_lane(Lane& ln, FrameDesc* frames, const int* idx, int n, const uint8_t qy[64],
+int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* next, const uint8_t qy[64],
                       const uint8_t qc[64], uint32_t flags) {
     const int S = (int)ln.slots.size();
-    auto frame = [&](int t) -> FrameDesc& { return frames[idx[t]]; };
+    std::vector<int> mine;  // batch indices of the frames this lane took, in its order
+    mine.reserve(total);
+    auto frame = [&](int t) -> FrameDesc& { return frames[mine[t]]; };
     int first_err = kOk;
     auto note = [&](int t, int st) {
         if (st && !frame(t).status) frame(t).status = st;
@@ -617,25 +656,52 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, const int* idx, int n, const 
         if (pool_) {
             Slot* sp = &s;
             const int dev = device_;
-            pool_->submit([this, sp, dev] {
-                hipSetDevice(dev);
-                sp->tables_status = build_tables(*sp, false);
-                sp->tables_done.store(1, std::memory_order_release);
-            });
+            // ready once the histograms are in (or after 2 ms, when build_tables'
+            // own bounded wait takes over and reports a failed stream)
+            sp->t_submit = std::chrono::steady_clock::now();
+            const auto due = sp->t_submit + std::chrono::milliseconds(2);
+            pool_->submit({[sp, due] {
+                               return __atomic_load_n(&sp->h_hist->seq, __ATOMIC_ACQUIRE) == sp->seq ||
+                                      std::chrono::steady_clock::now() > due;
+                           },
+                           [this, sp, dev] {
+                               sp->t_start = std::chrono::steady_clock::now();
+                               hipSetDevice(dev);
+                               sp->tables_status = build_tables(*sp, false);
+                               sp->t_done = std::chrono::steady_clock::now();
+                               sp->tables_done.store(1, std::memory_order_release);
+                           }});
         } else {
             s.tables_status = build_tables(s, true);
             s.tables_done.store(1, std::memory_order_release);
         }
     };
-    // diagnostic host trace: (iteration, point, us since the call)
-    std::vector<std::array<double, 3>> trace;
+    // diagnostic host trace: (iteration, point, us since the call, and at point 1 the
+    // awaited table job's submit / start / done times)
+    std::vector<std::array<double, 6>> trace;
     const auto t_call = std::chrono::steady_clock::now();
-    auto mark = [&](int i, int point) {
-        if (host_trace_file_)
-            trace.push_back({(double)i, (double)point,
-                             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count()});
+    auto us = [&](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::micro>(t - t_call).count();
     };
-    for (int i = 0; i < n + L + D; ++i) {
+    auto mark = [&](int i, int point, const Slot* job = nullptr) {
+        if (host_trace_file_)
+            trace.push_back({(double)i, (double)point, us(std::chrono::steady_clock::now()),
+                             job ? us(job->t_submit) : 0.0, job ? us(job->t_start) : 0.0,
+                             job ? us(job->t_done) : 0.0});
+    };
+    int n = 0;         // frames taken so far
+    bool open = true;  // the batch may still have frames
+    for (int i = 0;; ++i) {
+        if (open && i == n) {  // room for a new frame: take the batch's next one
+            const int g = next->fetch_add(1, std::memory_order_relaxed);
+            if (g < total) {
+                mine.push_back(g);
+                ++n;
+            } else {
+                open = false;
+            }
+        }
+        if (!open && i >= n + L + D) break;
         const int j = i - L, k = i - L - D;
         mark(i, 0);
         Slot* sj = nullptr;  // frame j, tables built, ready for its entropy kernels
@@ -647,8 +713,10 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, const int* idx, int n, const 
             }
             if (s.tables_status) note(j, s.tables_status);
             else sj = &s;
+            mark(i, 1, &s);
+        } else {
+            mark(i, 1);
         }
-        mark(i, 1);
         Slot* si = nullptr;  // frame i, whose histograms still need exporting
         bool imported = false;
         if (i < n) {
@@ -686,14 +754,21 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, const int* idx, int n, const 
     }
     // every output byte is in place: the stream's tail, awaited by spinning (a
     // blocking stream synchronisation adds tens of us of wake-up latency)
-    JPGE_HIP(hipEventRecord(ln.done, ln.stream));
-    JPGE_HIP(wait_event(ln.done));
-    mark(n + L + D, 5);
+    if (end_sync_ == 2) {
+        JPGE_HIP(hipStreamSynchronize(ln.stream));
+    } else {
+        JPGE_HIP(hipEventRecord(ln.done, ln.stream));
+        if (end_sync_ == 1) JPGE_HIP(hipEventSynchronize(ln.done));
+        else JPGE_HIP(wait_event(ln.done));
+    }
+    mark(n + L + D, 5);  // (n: this lane's frame count)
     if (host_trace_file_) {
         std::lock_guard<std::mutex> g(trace_mu_);
         if (FILE* f = std::fopen(host_trace_file_, "a")) {
-            for (const auto& t : trace) std::fprintf(f, "%d %d %.2f %d\n", (int)t[0], (int)t[1], t[2], ln.id);
-            std::fprintf(f, "-1 -1 0 %d\n", ln.id);
+            for (const auto& t : trace)
+                std::fprintf(f, "%d %d %.2f %d %.2f %.2f %.2f\n", (int)t[0], (int)t[1], t[2], ln.id, t[3], t[4], t[5]);
+            std::fprintf(f, "-1 -1 0 %d %.2f %.2f 0\n", ln.id, abs_us(t_call),
+                         abs_us(std::chrono::steady_clock::now()));
             std::fclose(f);
         }
     }

@@ -81,9 +81,9 @@ class Encoder {
     int import_tables_copy(Slot& s);
     int launch_entropy_phase(Slot& s, Slot* exp);
     int finish(Slot& s, FrameDesc& f, uint32_t flags);
-    // one lane's software pipeline over frames fr[idx[0..m)]
-    int run_lane(Lane& ln, FrameDesc* fr, const int* idx, int m, const uint8_t qy[64], const uint8_t qc[64],
-                 uint32_t flags);
+    // one lane's software pipeline over the frames it takes from fr[0..total) through `next`
+    int run_lane(Lane& ln, FrameDesc* fr, int total, std::atomic<int>* next, const uint8_t qy[64],
+                 const uint8_t qc[64], uint32_t flags);
 
     int device_ = 0;
     int timing_every_ = 0;
@@ -92,9 +92,10 @@ class Encoder {
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
-    int lookahead_ = 3;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
-    int drain_lag_ = 2;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
+    int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
+    int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables
+    int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
     bool nap_ = false;          // JPGE_NAP: lane threads sleep ~10 us between polls instead of spinning
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
@@ -104,7 +105,7 @@ class Encoder {
     KernelTimes times_;
     std::mutex times_mu_;  // finish() of several lanes
     std::mutex trace_mu_;
-    std::vector<std::unique_ptr<Lane>> lanes_;  // JPGE_LANES (default 2); lane 0 serves single-frame calls
+    std::vector<std::unique_ptr<Lane>> lanes_;  // JPGE_LANES (default 4: the device's hardware queues); lane 0 serves single-frame calls
 };
 
 }  // namespace jpge

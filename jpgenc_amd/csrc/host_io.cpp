@@ -1,4 +1,5 @@
 #include "host_io.hpp"
+#include "host_par.hpp"
 
 #include <algorithm>
 #include <cctype>
@@ -6,6 +7,7 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <thread>
 
 namespace jpge {
 
@@ -169,6 +171,13 @@ std::vector<uint8_t> jfif_headers(uint32_t rw, uint32_t rh, const uint8_t qy[64]
     return o;
 }
 
+namespace {
+int synth_threads(uint32_t h) {  // test-data synthesis: a few threads for large frames
+    const unsigned hw = std::thread::hardware_concurrency();
+    return h < 256 ? 1 : (int)std::min(8u, hw ? hw : 1u);
+}
+}  // namespace
+
 void synth_rgb8(uint64_t seed, uint32_t w, uint32_t h, int kind, uint8_t* out, size_t stride) {
     const uint64_t s = mix(seed);
     if (kind == 2) {
@@ -179,8 +188,7 @@ void synth_rgb8(uint64_t seed, uint32_t w, uint32_t h, int kind, uint8_t* out, s
     }
     const int px = (int)(s % 977) + 200, py = (int)((s >> 10) % 743) + 150;
     const int tx = (int)((s >> 20) % 23) + 9, ty = (int)((s >> 30) % 19) + 7;
-#pragma omp parallel for schedule(static)
-    for (int64_t yy = 0; yy < (int64_t)h; ++yy) {
+    parallel_for((long)h, synth_threads(h), [&](long yy) {
         const int y = (int)yy;
         uint8_t* row = out + (size_t)y * stride;
         for (uint32_t xu = 0; xu < w; ++xu) {
@@ -202,7 +210,7 @@ void synth_rgb8(uint64_t seed, uint32_t w, uint32_t h, int kind, uint8_t* out, s
                 row[x * 3 + c] = (uint8_t)std::min(255, std::max(0, val));
             }
         }
-    }
+    });
 }
 
 }  // namespace jpge

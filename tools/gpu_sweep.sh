@@ -1,7 +1,5 @@
-# ad-hoc GPU sweep (used through gpurun): the bench under a few settings
 mkdir -p gpurun_out
-nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null
-for cfg in "2 0" "2 1" "3 0" "3 1" "4 1" "2 0" "2 1" "3 0" "3 1" "4 1"; do set -- $cfg
-  r=$(JPGE_LANES=$1 JPGE_NAP=$2 timeout -k 10 200 python bench.py --no-cpu-baseline 2>>gpurun_out/sweep_err.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read().splitlines()[-1]); print(d['value'], d['ms_per_step'])") || exit 1
-  echo "lanes=$1 nap=$2 $r"
+for cfg in "4 2 1" "5 2 1" "6 2 1" "8 2 1" "4 3 1" "4 2 2" "6 2 1" "4 2 1"; do set -- $cfg
+  res=$(JPGE_LANES=$1 JPGE_LOOKAHEAD=$2 JPGE_DRAIN_LAG=$3 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 2>>gpurun_out/sweep_err.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read().splitlines()[-1]); print(d['value'], d['step_ms'], d['host_cpu']['cpus_used'])") || exit 1
+  echo "lanes=$1 L=$2 D=$3 $res"
 done
