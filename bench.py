@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--width", type=int, default=W4K)
     ap.add_argument("--height", type=int, default=H4K)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solo-batches", type=int, default=2,
+                    help="batches through a 1-lane encoder after the timed region (kernel times alone; 0 = skip)")
+    ap.add_argument("--lanes", type=int, default=0, help="encoder lanes (0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
@@ -172,7 +175,7 @@ def main():
     import jpgenc_amd as J
 
     torch.cuda.set_device(local)
-    enc = J.Encoder(local)
+    enc = J.Encoder(local, lanes=args.lanes)
     W, H, F = args.width, args.height, args.frames
     pitch = W * 3
     cap = J.max_jpeg_bytes(W, H)
@@ -229,24 +232,52 @@ def main():
     pixels = sum_over_ranks(pg, float(W * H * F * args.steps))
     value = pixels / dt_max / 1e6
 
+    # Solo pass (after the timed region, not part of `value`): the same frames through
+    # a single-lane encoder with events around every frame's kernels, so each kernel's
+    # duration is its own, without other lanes' kernels beside it.
+    tm_solo = None
+    if args.solo_batches > 0 and not args.no_kernel_events:
+        solo = J.Encoder(local, lanes=1)
+        solo.encode_batch_dev(frames, outd, quality=args.quality)
+        solo.set_timing(1)
+        solo.reset_timing()
+        for _ in range(args.solo_batches):
+            solo.encode_batch_dev(frames, outd, quality=args.quality)
+        tm_solo = solo.timing()
+        solo.close()
+
     # per-kernel rooflines (HBM-bound integer/fp64 work; algorithmic bytes per launch)
-    nfr = max(1, tm["frames"])
     npx = W * H
     avg_jpeg = total_bytes / (args.steps * F)
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H)
-    stage_defs = [
-        ("fdct_kernel", tm["fdct_sum"] / nfr, 6.0 * npx, "RGB8 read 3 B/px + int16 coefficients written 3 B/px"),
-        ("stats_kernel", tm["dc_stats_sum"] / nfr, 3.0 * npx, "coefficients read 3 B/px"),
-        ("entropy_kernel", tm["entropy_sum"] / nfr, 3.0 * npx + avg_jpeg,
-         "coefficients read 3 B/px + entropy-coded bytes written"),
-    ]
-    stages = {}
-    for name, ms, alg, what in stage_defs:
-        ach = alg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # (0: --no-kernel-events)
-        stages[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
-                        "alg_bytes_per_launch": int(alg), "alg_bytes": what, "avg_kernel_ms": round(ms, 5)}
+    alg = {
+        "fdct_kernel": (6.0 * npx, "RGB8 read 3 B/px + int16 coefficients written 3 B/px"),
+        "stats_kernel": (3.0 * npx, "coefficients read 3 B/px"),
+        "entropy_kernel": (3.0 * npx + avg_jpeg, "coefficients read 3 B/px + entropy-coded bytes written"),
+    }
+
+    def rooflines(tm):
+        nfr = max(1, tm["frames"])
+        ms = {"fdct_kernel": tm["fdct_sum"] / nfr, "stats_kernel": tm["dc_stats_sum"] / nfr,
+              "entropy_kernel": tm["entropy_sum"] / nfr}
+        out = {}
+        for name, (b, what) in alg.items():
+            ach = b / (ms[name] * 1e-3) / 1e9 if ms[name] > 0 else 0.0  # (0: --no-kernel-events)
+            out[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
+                         "alg_bytes_per_launch": int(b), "alg_bytes": what, "avg_kernel_ms": round(ms[name], 5),
+                         "timed_launches": tm["frames"]}
+        return out
+
+    stages = rooflines(tm)  # in situ: the timed region, lanes side by side
+    stages_solo = rooflines(tm_solo) if tm_solo else None
     dominant = max(stages, key=lambda k: stages[k]["avg_kernel_ms"])
+    # whole pipeline: every kernel's algorithmic bytes per frame, over the wall time
+    pipe_bytes = sum(b for b, _ in alg.values())
+    pipe_ach = pipe_bytes * F * args.steps * world / dt_max / 1e9
+    pipeline = {"bound": "hbm", "achieved": round(pipe_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(pipe_ach / HBM_PEAK_GBS, 4), "alg_bytes_per_frame": int(pipe_bytes),
+                "note": "sum of the kernels' algorithmic bytes per frame x frames / wall time (per GPU)"}
 
     if rank == 0:
         line = {
@@ -270,11 +301,17 @@ def main():
                 "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
                 "avg_jpeg_bytes": int(total_bytes / (args.steps * F)),
             },
-            "roofline": dict(kernel=dominant, **stages[dominant]),
-            # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px)
-            "roofline_dct_stage": dict(kernel="fdct_kernel", **stages["fdct_kernel"]),
+            # dominant kernel, timed in situ (HIP events on its lane's stream, lanes side by side)
+            "roofline": dict(kernel=dominant, timing="in situ", **stages[dominant]),
+            # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px): the kernel alone
+            "roofline_dct_stage": dict(kernel="fdct_kernel", timing="solo", **stages_solo["fdct_kernel"])
+            if stages_solo else dict(kernel="fdct_kernel", timing="in situ", **stages["fdct_kernel"]),
+            "roofline_pipeline": pipeline,
             "stages": stages,
-            "kernel_events": f"HIP events around every {args.event_every}th frame's kernels on the encoder streams",
+            "stages_solo": stages_solo,
+            "kernel_events": f"in situ: HIP events around every {args.event_every}th frame's kernels on its lane's "
+                             f"stream; solo: every frame of {args.solo_batches} batches on a 1-lane encoder after "
+                             f"the timed region",
             "step_ms": {"min": round(min(step_t) * 1e3, 3), "median": round(sorted(step_t)[len(step_t) // 2] * 1e3, 3),
                         "max": round(max(step_t) * 1e3, 3)},
             "lanes": enc.lanes(),

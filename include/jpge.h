@@ -70,6 +70,9 @@ int jpge_device_count(int* n);
 
 /* Context lifetime (replaces nothing in the reference: its encoder is stateless). */
 int jpge_open(int device, jpge_ctx** ctx);
+/* jpge_open with an explicit lane count (0 = JPGE_LANES or the default 4; at most 8;
+ * 1 = a single pipeline, e.g. to time kernels without other frames beside them). */
+int jpge_open_ex(int device, int lanes, jpge_ctx** ctx);
 int jpge_close(jpge_ctx* ctx);
 /* Kernel timing with HIP events on the encoder's stream: every = 0 off, N >= 1
  * times the kernels of every N-th frame (1 = all; events cost GPU time). */

@@ -30,7 +30,7 @@ STATUS = {
 
 # every symbol include/jpge.h declares (checked by tests/test_abi.py)
 EXPORTS = (
-    "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_close", "jpge_set_timing",
+    "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_open_ex", "jpge_close", "jpge_set_timing",
     "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_synth_rgb8", "jpge_arai_constants",
@@ -72,6 +72,7 @@ def lib() -> ctypes.CDLL:
         L.jpge_strerror.restype = ctypes.c_char_p
         L.jpge_strerror.argtypes = [i32]
         L.jpge_open.argtypes = [i32, ctypes.POINTER(vp)]
+        L.jpge_open_ex.argtypes = [i32, i32, ctypes.POINTER(vp)]
         L.jpge_close.argtypes = [vp]
         L.jpge_set_timing.argtypes = [vp, i32]
         L.jpge_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
@@ -201,9 +202,10 @@ class Encoder:
     """One GPU context (jpge_open).  Host-array methods copy in/out; the `*_dev`
     variants take device pointers (ints) for HBM-resident frames."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lanes: int = 0):
+        """lanes: concurrent pipelines on the device (0 = JPGE_LANES or the default 4)."""
         self._ctx = ctypes.c_void_p()
-        _check(lib().jpge_open(int(device), ctypes.byref(self._ctx)), f"jpge_open({device})")
+        _check(lib().jpge_open_ex(int(device), int(lanes), ctypes.byref(self._ctx)), f"jpge_open({device})")
         self.device = device
         self._qcache = {}     # quality -> (qy, qc) byte tables
         self._desc = None     # (key, Frame array) of the last device batch

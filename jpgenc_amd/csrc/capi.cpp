@@ -55,12 +55,15 @@ int jpge_device_count(int* n) {
     return JPGE_OK;
 }
 
-int jpge_open(int device, jpge_ctx** ctx) {
+int jpge_open(int device, jpge_ctx** ctx) { return jpge_open_ex(device, 0, ctx); }
+
+int jpge_open_ex(int device, int lanes, jpge_ctx** ctx) {
     if (!ctx) return JPGE_E_ARG;
     *ctx = nullptr;
+    if (lanes < 0) return JPGE_E_ARG;
     std::unique_ptr<jpge_ctx> c(new (std::nothrow) jpge_ctx());
     if (!c) return JPGE_E_INTERNAL;
-    int st = jpge::Encoder::open(device, c->enc);
+    int st = jpge::Encoder::open(device, c->enc, lanes);
     if (st) return st;
     *ctx = c.release();
     return JPGE_OK;

@@ -291,7 +291,7 @@ size_t Encoder::max_jpeg_bytes(uint32_t w, uint32_t h) {
     return 2048 + (size_t)g.nblocks() * 2 * 209 + 16;
 }
 
-int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
+int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return kErrNoDevice;
     if (device < 0 || device >= n) return kErrNoDevice;
@@ -317,7 +317,9 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out) {
     // i's tables while the GPU works on later frames.  Lanes run frames side by side,
     // so one lane's kernels fill another's launch tails and latency-bound phases
     // (4 lanes = the hardware queues HIP opens per process; measured best).
-    const int nlanes = e->stamps_file_ ? 1 : env_int("JPGE_LANES", 4, 1, kMaxLanes);
+    const int nlanes = e->stamps_file_ ? 1
+                       : lanes > 0   ? std::min(lanes, kMaxLanes)
+                                     : env_int("JPGE_LANES", 4, 1, kMaxLanes);
     const int nslots = e->lookahead_ + e->drain_lag_ + 1;  // a slot is reused after its drain
     for (int l = 0; l < nlanes; ++l) {
         std::unique_ptr<Lane> ln(new Lane());

@@ -41,7 +41,8 @@ struct KernelTimes {  // milliseconds of the last timed frame (HIP events on the
 
 class Encoder {
   public:
-    static int open(int device, std::unique_ptr<Encoder>& out);
+    // lanes <= 0: JPGE_LANES or the default (4)
+    static int open(int device, std::unique_ptr<Encoder>& out, int lanes = 0);
     ~Encoder();
 
     int encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags);
