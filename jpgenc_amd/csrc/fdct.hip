@@ -42,19 +42,20 @@ __device__ __forceinline__ void arai8(const double x[8], double o[8]) {
 
 // quantize, Coding.hpp:92-94: (int)std::round(d / q) — correctly rounded fp64
 // division, then round half away from zero.  Fast path: r = d * (1/q) is within
-// ~2 ulp of the true quotient, so round(r) == round(fl(d/q)) unless r lies within
-// 2^-30 of a half-integer (|q| >= 1, |d/q| < 2^20 keep that bound far above the
-// error); those rare cases take the exact division.  Integer boundaries are
-// harmless: a quotient on either side of k rounds to k either way.
-__device__ __forceinline__ int quant1(double d, double q, double invq) {
+// 2^-52 |r| of the true quotient and |r| <= |d| < 2^15 (q >= 1, 8-bit samples), so
+// unless r lies within 2^-30 of a half-integer, rint(r) (ties-to-even, but r is no
+// tie) equals the reference's integer; integer boundaries are harmless (a quotient
+// on either side of k rounds to k either way).  e = r - rint(r) is exact, so a lane
+// near a half-integer is flagged by |e| > 0.5 - 2^-30 and the whole row is redone
+// by exact division (rare; one branch per row).
+__device__ __forceinline__ int quant_fast(double d, double invq, bool& near_half) {
     const double r = d * invq;
-    const double a = __builtin_fabs(r);
-    const double fl = __builtin_floor(a);
-    const double f = a - fl;
-    if (__builtin_fabs(f - 0.5) < 0x1p-30 || a >= 0x1p20) return (int)round(d / q);
-    const int n = (int)fl + (f > 0.5 ? 1 : 0);
-    return r < 0 ? -n : n;
+    const double k = __builtin_rint(r);
+    near_half |= __builtin_fabs(r - k) > 0.5 - 0x1p-30;
+    return (int)k;
 }
+
+__device__ __forceinline__ int quant_exact(double d, double q) { return (int)round(d / q); }
 
 constexpr int kK1Threads = 256;  // 4 waves, one 4-MCU tile each
 constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
@@ -219,9 +220,13 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
             for (int i = 0; i < 8; ++i) x[i] = tb[i * kTmpRow + j];
             arai8(x, o);  // o[u] = y(j, u)
             int qv[8];
+            bool near_half = false;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                qv[u] = quant1(o[u], lds.q[qb][j * kQRow + u], lds.invq[qb][j * kQRow + u]);
+            for (int u = 0; u < 8; ++u) qv[u] = quant_fast(o[u], lds.invq[qb][j * kQRow + u], near_half);
+            if (__builtin_amdgcn_ballot_w64(near_half)) {  // wave-uniform: a real branch, not predication
+#pragma unroll
+                for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], lds.q[qb][j * kQRow + u]);
+            }
             if (m < nvalid) {
                 const uint64_t blk = ((uint64_t)mrow * mw + mcol0 + m) * 6 + slot;
                 uint4 pk;
