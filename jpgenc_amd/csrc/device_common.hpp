@@ -136,9 +136,13 @@ struct TileRegs {
 
 // DC of the chain predecessor of block b0+blk (0 for a chain's first block), from
 // the staged tile or the 6 DCs staged before it.
-__device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, const int* prevdc) {
+__device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, const int* prevdc,
+                                       const DcSeed& seed) {
     const int64_t pg = dc_pred_index(b0 + blk);
-    if (pg < 0) return 0;
+    if (pg < 0) {  // first MCU: the chain starts at 0, or at the previous stripe's last DC
+        const int k = (int)((b0 + blk) % 6);
+        return seed.v[k == 0 ? 0 : k - 3];
+    }
     if (pg >= (int64_t)b0) return zz[(pg - (int64_t)b0) * kZzStride];
     return prevdc[pg - ((int64_t)b0 - 6)];
 }

@@ -97,13 +97,17 @@ constexpr size_t kHdrMax = 4096;           // headers SOI .. SOS (<= 20 + 2*69 +
 
 // Control block, zeroed at the start of every frame by the first kernel (K1).
 struct CtlLayout {
-    size_t cnt, key, rec, total;
+    size_t cnt, key, rec, total;  // [0, total): zeroed by K1 every frame
+    size_t place, summary, alloc;  // not zeroed (written before they are read)
     explicit CtlLayout(uint32_t ntiles) {  // (entropy workgroups <= entropy tiles)
         size_t o = 0;
         cnt = o; o += align_up((size_t)kHistReplicas * 4 * 256 * 4, 256);
         key = o; o += align_up(4 * 256 * 8, 256);
         rec = o; o += align_up((size_t)ntiles * kEntropyRecordBytes, 256);
         total = o;
+        place = o; o += align_up((size_t)ntiles * sizeof(WgPlace), 256);
+        summary = o; o += 256;
+        alloc = o;
     }
 };
 
@@ -307,6 +311,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
     e->nap_ = env_int("JPGE_NAP", 0, 0, 1) != 0;
     e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
+    e->ext_place_ = env_int("JPGE_EXT_PLACE", 0, 0, 1) != 0;
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -392,10 +397,10 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         JPGE_HIP(hipMalloc((void**)&s.d_ubuf, ubuf));
         s.cap_ubuf = ubuf;
     }
-    if (L.total > s.cap_ctl) {
+    if (L.alloc > s.cap_ctl) {
         hipFree(s.d_ctl); s.d_ctl = nullptr; s.cap_ctl = 0;
-        JPGE_HIP(hipMalloc((void**)&s.d_ctl, L.total));
-        s.cap_ctl = L.total;
+        JPGE_HIP(hipMalloc((void**)&s.d_ctl, L.alloc));
+        s.cap_ctl = L.alloc;
     }
     if (in_bytes > s.cap_in) {
         hipFree(s.d_in); s.d_in = nullptr; s.cap_in = 0;
@@ -536,6 +541,8 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
     e.hdr_len = s.hdr_len;
     e.out_cap = s.out_cap;
     e.rec = s.d_ctl + L.rec;
+    e.place = reinterpret_cast<WgPlace*>(s.d_ctl + L.place);
+    if (ext_place_) e.flags |= kExtPlace;
     e.host_result = s.d_result_host;
     e.seq = s.seq;
     s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1)

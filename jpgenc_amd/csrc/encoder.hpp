@@ -96,6 +96,7 @@ class Encoder {
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables
+    bool ext_place_ = false;    // JPGE_EXT_PLACE: entropy placement by the scan kernel at every size (tests)
     int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
     bool nap_ = false;          // JPGE_NAP: lane threads sleep ~10 us between polls instead of spinning
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps

@@ -111,7 +111,8 @@ struct PartCoder {
     bool active;
 };
 
-__device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int nb, int blk, int part) {
+__device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int nb, int blk, int part,
+                                                const DcSeed& seed) {
     PartCoder c;
     c.part = part;
     c.active = blk < nb;
@@ -121,7 +122,7 @@ __device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int
     c.mask = c.active ? L.bmask[blk] : 0ull;
     c.pv.load(L.u.zz, c.mask, blk, part, c.active);
     // DC difference to the chain predecessor, Image.cpp:638-678
-    c.dcdiff = (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc) : 0;
+    c.dcdiff = (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc, seed) : 0;
     return c;
 }
 
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         JPGE_ACC(0, tq);
         uint32_t n;  // bits of this lane's part
         {
-            const PartCoder pc = make_coder(L, b0, nb, blk, part);
+            const PartCoder pc = make_coder(L, b0, nb, blk, part, a.seed);
             SlotSink ss;
             ss.init(L.slot + tid);
             n = code_part(pc, ss);
@@ -288,6 +289,141 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     JPGE_STAMP(2);
 }
 
+// ---- record scan: bit offsets, byte splits and 0xFF prefixes ----
+// A byte belongs to the workgroup holding its last bit.  The byte split between
+// records k-1 and k (alignment b_k = P_k & 7 != 0) is rebuilt from k-1's last b_k
+// bits and k's first 8 - b_k bits and counted for k; for k == 0 it is the byte the
+// stripe shares with the previous stripe (a.head_split).  The image's last record
+// owns the 1-filled final byte.
+struct RecView {
+    const uint8_t* base;
+    uint32_t G;
+    __device__ __forceinline__ const uint32_t* operator()(uint32_t k) const {
+        return reinterpret_cast<const uint32_t*>(base + (uint64_t)k * kEntropyRecordBytes);
+    }
+};
+
+__device__ __forceinline__ uint32_t split_bits(uint32_t ptail, uint32_t head, uint32_t b) {  // 0 < b < 8
+    return (((ptail & ((1u << b) - 1)) << (8 - b)) | ((head & 0xFF) >> b)) & 0xFF;
+}
+__device__ __forceinline__ uint32_t split_byte(const RecView& R, uint32_t k, uint32_t b, const EntropyArgs& a) {
+    if (k == 0) return a.head_split;
+    return split_bits((R(k - 1)[kRecEdge] >> 8) & 0xFF, R(k)[kRecEdge], b);
+}
+__device__ __forceinline__ uint32_t fill_byte(uint32_t eb, uint32_t edge) {  // Bitstream::fill, BitstreamGeneric.hpp:243-248
+    return ((((edge >> 8) & ((1u << eb) - 1)) << (8 - eb)) | (0xFFu >> eb)) & 0xFF;
+}
+// 0xFF bytes owned by record k when its stream starts at global bit p
+__device__ __forceinline__ uint32_t owned_ff(const RecView& R, uint32_t k, uint64_t p, const EntropyArgs& a) {
+    const uint32_t* r = R(k);
+    const uint32_t b = (uint32_t)(p & 7), edge = r[kRecEdge];
+    uint32_t f = r[b];
+    if (b) f += split_byte(R, k, b, a) == 0xFF;
+    const uint32_t eb = (uint32_t)((p + r[kRecBits]) & 7);
+    if (k == R.G - 1 && (a.flags & kStripeLast) && eb) f += fill_byte(eb, edge) == 0xFF;
+    return f;
+}
+
+// Thread t takes records [t*per, (t+1)*per); fn(k, P, Q, owned) for each of them.
+template <int kWaves, class F>
+__device__ __forceinline__ void scan_records(const EntropyArgs& a, const RecView& R, uint32_t* wsum, int tid, F&& fn) {
+    const int lane = tid & 63, wv = tid >> 6;
+    const uint32_t per = (R.G + kWaves * 64 - 1) / (kWaves * 64);
+    const uint32_t k0 = min(R.G, tid * per), k1 = min(R.G, k0 + per);
+    uint64_t lsum = 0;
+    for (uint32_t k = k0; k < k1; ++k) lsum += R(k)[kRecBits];
+    uint64_t ltot;
+    const uint64_t pbase = a.p_ext + block_scan<kWaves>(lsum, wsum, lane, wv, ltot);
+    uint64_t fsum = 0;
+    {
+        uint64_t p = pbase;
+        for (uint32_t k = k0; k < k1; ++k) {
+            fsum += owned_ff(R, k, p, a);
+            p += R(k)[kRecBits];
+        }
+    }
+    uint64_t ftot;
+    const uint64_t fbase = a.q_ext + block_scan<kWaves>(fsum, wsum, lane, wv, ftot);
+    uint64_t p = pbase, q = fbase;
+    for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t o = owned_ff(R, k, p, a);
+        fn(k, p, q, o);
+        q += o;
+        p += R(k)[kRecBits];
+    }
+}
+
+__device__ __forceinline__ WgPlace make_place(const RecView& R, uint32_t k, uint64_t p, uint64_t q, uint32_t owned,
+                                              const EntropyArgs& a) {
+    const uint32_t* r = R(k);
+    const uint32_t b = (uint32_t)(p & 7), edge = r[kRecEdge];
+    const uint32_t eb = (uint32_t)((p + r[kRecBits]) & 7);
+    WgPlace w;
+    w.P = p;
+    w.Q = q;
+    w.ftotal = owned;
+    w.split = b ? split_byte(R, k, b, a) : 0u;
+    w.fill = (k == R.G - 1 && (a.flags & kStripeLast) && eb) ? fill_byte(eb, edge) : 0u;
+    w.pad = 0;
+    return w;
+}
+
+constexpr int kScanThreads = 1024;
+
+// entropy_scan_kernel — one workgroup over all G records.  Place mode: every
+// workgroup's WgPlace (large grids, stripes).  Summary mode: the stripe's bits,
+// edge bytes and its internal 0xFF count at each of the 8 start alignments.
+__global__ __launch_bounds__(kScanThreads) void entropy_scan_kernel(EntropyArgs a, uint32_t G, int summary) {
+    __shared__ uint32_t wsum[2 * (kScanThreads / 64)];
+    __shared__ uint32_t tot8[8];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const RecView R{a.rec, G};
+    if (!summary) {
+        scan_records<kScanThreads / 64>(a, R, wsum, tid, [&](uint32_t k, uint64_t p, uint64_t q, uint32_t o) {
+            a.place[k] = make_place(R, k, p, q, o, a);
+        });
+        return;
+    }
+    if (tid < 8) tot8[tid] = 0;
+    const uint32_t per = (G + kScanThreads - 1) / kScanThreads;
+    const uint32_t k0 = min(G, tid * per), k1 = min(G, k0 + per);
+    uint64_t lsum = 0;
+    for (uint32_t k = k0; k < k1; ++k) lsum += R(k)[kRecBits];
+    uint64_t total;
+    const uint64_t pbase = block_scan<kScanThreads / 64>(lsum, wsum, lane, wv, total);  // stripe-local
+    uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // c[al]: stripe starting at bit al (mod 8)
+    {
+        uint64_t p = pbase;
+        for (uint32_t k = k0; k < k1; ++k) {
+            const uint32_t* r = R(k);
+#pragma unroll
+            for (int al = 0; al < 8; ++al) {
+                const uint32_t b = (uint32_t)((p + al) & 7);
+                c[al] += r[b];
+                if (b && k > 0) c[al] += split_bits((R(k - 1)[kRecEdge] >> 8) & 0xFF, r[kRecEdge], b) == 0xFF;
+            }
+            p += r[kRecBits];
+        }
+    }
+#pragma unroll
+    for (int al = 0; al < 8; ++al) {
+        uint32_t v = c[al];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+        if (lane == 0 && v) atomicAdd(&tot8[al], v);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        StripeSummary sm;
+        sm.bits = total;
+#pragma unroll
+        for (int al = 0; al < 8; ++al) sm.ff[al] = tot8[al];
+        sm.head = R(0)[kRecEdge] & 0xFF;
+        sm.tail = (R(G - 1)[kRecEdge] >> 8) & 0xFF;
+        *a.summary = sm;
+    }
+}
+
 struct PackLds {
     uint8_t ob[2 * kChunk + 8];  // stuffed output of one round
     uint32_t wsum[2 * kK3Waves];  // (room for 64-bit scans)
@@ -300,66 +436,36 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t wg = blockIdx.x, G = gridDim.x;
     const bool last = wg == G - 1;
+    const bool eoi = last && (a.flags & kStripeLast);
     JPGE_STAMP(0);
-    if (wg == 0) {  // the headers (SOI .. SOS) travel behind the tables
+    if (wg == 0 && (a.flags & kStripeFirst)) {  // the headers (SOI .. SOS) travel behind the tables
         const uint8_t* hdr = reinterpret_cast<const uint8_t*>(a.tables + 1024);
         for (uint32_t i = tid; i < a.hdr_len; i += kK3Threads) a.out[i] = hdr[i];
     }
 
-    // ---- scan of all records: this workgroup's bit offset P and 0xFF prefix Q ----
-    // Thread t takes records [t*per, (t+1)*per).  The byte split between records
-    // k-1 and k (alignment b_k = P_k & 7 != 0) is rebuilt from k-1's last b_k bits
-    // and k's first 8 - b_k bits and counted for k (its owner); the last record's
-    // 1-filled final byte is counted for it.
-    const uint32_t per = (G + kK3Threads - 1) / kK3Threads;
-    const uint32_t k0 = min(G, tid * per), k1 = min(G, k0 + per);
-    auto rec = [&](uint32_t k) { return reinterpret_cast<const uint32_t*>(a.rec + (uint64_t)k * kEntropyRecordBytes); };
-    auto split_byte = [&](uint32_t k, uint32_t b, uint32_t edge) -> uint32_t {  // b != 0, k > 0
-        const uint32_t ptail = (rec(k - 1)[kRecEdge] >> 8) & 0xFF;
-        return (((ptail & ((1u << b) - 1)) << (8 - b)) | ((edge & 0xFF) >> b)) & 0xFF;
-    };
-    auto fill_byte = [&](uint32_t eb, uint32_t edge) -> uint32_t {  // Bitstream::fill, BitstreamGeneric.hpp:243-248
-        return ((((edge >> 8) & ((1u << eb) - 1)) << (8 - eb)) | (0xFFu >> eb)) & 0xFF;
-    };
-    // 0xFF bytes owned by record k when its stream starts at global bit p
-    auto owned_ff = [&](uint32_t k, uint64_t p) -> uint32_t {
-        const uint32_t* r = rec(k);
-        const uint32_t b = (uint32_t)(p & 7), edge = r[kRecEdge];
-        uint32_t f = r[b];
-        if (b && k > 0) f += split_byte(k, b, edge) == 0xFF;
-        const uint32_t eb = (uint32_t)((p + r[kRecBits]) & 7);
-        if (k == G - 1 && eb) f += fill_byte(eb, edge) == 0xFF;
-        return f;
-    };
-    uint64_t lsum = 0;
-    for (uint32_t k = k0; k < k1; ++k) lsum += rec(k)[kRecBits];
-    uint64_t ltot;
-    const uint64_t pbase = block_scan<kK3Waves>(lsum, S.wsum, lane, wv, ltot);
-    uint64_t fsum = 0;
-    {
-        uint64_t p = pbase;
-        for (uint32_t k = k0; k < k1; ++k) {
-            fsum += owned_ff(k, p);
-            p += rec(k)[kRecBits];
+    // ---- this workgroup's placement: from the scan kernel, or scanned here ----
+    const RecView R{a.rec, G};
+    if (a.flags & kExtPlace) {
+        if (tid == 0) {
+            const WgPlace w = a.place[wg];
+            S.P = w.P;
+            S.Q = w.Q;
+            S.ftotal = w.ftotal;
+            S.split = w.split;
+            S.fill = w.fill;
+            S.Lb = R(wg)[kRecBits];
         }
-    }
-    uint64_t ftot;
-    const uint64_t fbase = block_scan<kK3Waves>(fsum, S.wsum, lane, wv, ftot);
-    if (k0 <= wg && wg < k1) {  // this workgroup's record: offsets and edge bytes
-        uint64_t p = pbase, q = fbase;
-        for (uint32_t k = k0; k < wg; ++k) {
-            q += owned_ff(k, p);
-            p += rec(k)[kRecBits];
-        }
-        const uint32_t* r = rec(wg);
-        const uint32_t b = (uint32_t)(p & 7), bits = r[kRecBits], edge = r[kRecEdge];
-        const uint32_t eb = (uint32_t)((p + bits) & 7);
-        S.P = p;
-        S.Q = q;
-        S.Lb = bits;
-        S.ftotal = owned_ff(wg, p);
-        S.split = (b && wg > 0) ? split_byte(wg, b, edge) : 0u;
-        S.fill = (last && eb) ? fill_byte(eb, edge) : 0u;
+    } else {
+        scan_records<kK3Waves>(a, R, S.wsum, tid, [&](uint32_t k, uint64_t p, uint64_t q, uint32_t o) {
+            if (k != wg) return;
+            const WgPlace w = make_place(R, k, p, q, o, a);
+            S.P = w.P;
+            S.Q = w.Q;
+            S.ftotal = w.ftotal;
+            S.split = w.split;
+            S.fill = w.fill;
+            S.Lb = R(k)[kRecBits];
+        });
     }
     __syncthreads();
     JPGE_STAMP(1);
@@ -369,9 +475,9 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
     const uint32_t b = (uint32_t)(P & 7), Lb = S.Lb, ftotal = S.ftotal;
     const uint32_t nc = (b + Lb) >> 3;  // complete output bytes
     const uint32_t eb = (b + Lb) & 7;   // bits in the byte after them
-    const uint32_t n_own = nc + ((last && eb) ? 1u : 0u);
+    const uint32_t n_own = nc + ((eoi && eb) ? 1u : 0u);
     const uint64_t D0 = a.hdr_len + (P >> 3) + S.Q;
-    const uint64_t ntot = (uint64_t)n_own + ftotal + (last ? 2u : 0u);
+    const uint64_t ntot = (uint64_t)n_own + ftotal + (eoi ? 2u : 0u);
     const bool fits = D0 + ntot <= a.out_cap;
     const uint32_t split = S.split, fill = S.fill;
     const uint32_t* R32 = reinterpret_cast<const uint32_t*>(a.ubuf + (uint64_t)wg * kEntropyRegionBytes);
@@ -394,7 +500,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
                 prev = cur;
             }
             if (j0 == 0 && b) y[0] = (y[0] & 0x00FFFFFFu) | (split << 24);
-            if (last && eb && n_own - 1 < j0 + kWin) {
+            if (eoi && eb && n_own - 1 < j0 + kWin) {
                 const uint32_t q = n_own - 1 - j0, sh = 24 - 8 * (q & 3);
 #pragma unroll
                 for (int m = 0; m < kWinWords; ++m)
@@ -437,11 +543,14 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
         __syncthreads();  // ob is rewritten by the next round
     }
     if (last && tid == 0) {
-        uint64_t len = 0;
-        if (fits) {  // EOI, Image.cpp:1003-1005
-            a.out[d] = 0xFF;
-            a.out[d + 1] = 0xD9;
-            len = d + 2;
+        uint64_t len = 0;  // end of the image (EOI written) or of the stripe's bytes
+        if (fits) {
+            if (eoi) {  // EOI, Image.cpp:1003-1005
+                a.out[d] = 0xFF;
+                a.out[d + 1] = 0xD9;
+                d += 2;
+            }
+            len = d;
         }
         // length and no-space flag straight into mapped host memory: the last
         // workgroup's end offset bounds every workgroup's, so it alone decides
@@ -473,6 +582,34 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
+    if (G > kInlineScanMaxWgs || (a.flags & kExtPlace)) {
+        if (!a.place) return hipErrorInvalidValue;
+        b.flags |= kExtPlace;
+        hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
+    const uint32_t G = entropy_grid(a.g, a.wgs);
+    if (!a.summary) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, a, G, 1);
+    return hipGetLastError();
+}
+
+hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s) {
+    const uint32_t G = entropy_grid(a.g, a.wgs);
+    if (!a.place) return hipErrorInvalidValue;
+    EntropyArgs b = a;
+    b.flags |= kExtPlace;
+    hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
     return hipGetLastError();
 }

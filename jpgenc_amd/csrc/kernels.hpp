@@ -62,12 +62,47 @@ struct FdctArgs {
     uint64_t* dbg;   // diagnostic phase stamps (JPGE_STAMPS builds), else unused
 };
 
+// Stripe context of a frame (a row stripe of a larger image); the
+// defaults describe a whole frame.
+struct DcSeed {
+    int v[3] = {0, 0, 0};  // DC chain predecessors of the first Y / Cb / Cr block (Image.cpp:638-678)
+};
+
 struct StatsArgs {
     const int16_t* coef;
     Geometry g;
     HistPtrs hist;
+    DcSeed seed;
+    // first-occurrence key bases in the whole image's texts (Image.cpp:888-906):
+    // Y raster index of the stripe's first Y block, Cb raster index of its first
+    // Cb block, and the image's Cb block count (every Cr key follows all Cb keys)
+    uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
     uint64_t* dbg;
 };
+
+// Where each entropy workgroup's bytes go (entropy_scan_kernel -> pack kernel).
+struct alignas(16) WgPlace {
+    uint64_t P;       // global bit offset of the workgroup's stream
+    uint64_t Q;       // 0x00 stuffing bytes before its first owned byte
+    uint32_t ftotal;  // 0xFF bytes it owns (its stuffing count)
+    uint32_t split;   // value of its first byte when shared with the predecessor (P & 7 != 0)
+    uint32_t fill;    // its 1-filled final byte (the image's last workgroup)
+    uint32_t pad;
+};
+
+// A stripe's entropy summary (entropy_scan_kernel, summary mode): enough for the
+// stripes to place their bytes after one all-gather.
+struct StripeSummary {
+    uint64_t bits;   // length of the stripe's stream
+    uint32_t ff[8];  // ff[a]: 0xFF bytes wholly inside the stripe when it starts at bit a (mod 8),
+                     // the byte shared with the previous stripe and the final fill byte excluded
+    uint32_t head;   // its first 8 bits (MSB-first byte)
+    uint32_t tail;   // its last 8 bits
+};
+
+constexpr uint32_t kStripeFirst = 1u;  // holds the image's first bit: writes the headers
+constexpr uint32_t kStripeLast = 2u;   // holds the last bit: 1-fill and EOI
+constexpr uint32_t kExtPlace = 4u;     // pack kernel reads WgPlace (entropy_scan_kernel) instead of scanning
 
 struct EntropyArgs {
     const int16_t* coef;
@@ -90,6 +125,14 @@ struct EntropyArgs {
     uint64_t exp_seqv;
     uint32_t wgs;            // workgroup count override (0 = automatic; tests)
     uint32_t diag;           // diagnostic switches (JPGE_DIAG; 0 in production)
+    DcSeed seed;             // DC chain predecessors (stripes)
+    // placement (stripes / large grids): stream starts at global bit p_ext with q_ext
+    // stuffing bytes before it; head_split = its first byte when p_ext & 7 != 0
+    uint64_t p_ext = 0, q_ext = 0;
+    uint32_t head_split = 0;
+    uint32_t flags = kStripeFirst | kStripeLast;
+    WgPlace* place = nullptr;          // [entropy_grid] (kExtPlace)
+    StripeSummary* summary = nullptr;  // summary mode output
     uint64_t* dbg;
 };
 
@@ -113,6 +156,13 @@ hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
 // [4][256] summed counts and keys into (mapped) host memory, then *host_seq = seq
 hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
                               uint64_t seq, hipStream_t s);
+// code + pack kernels (with the placement scan between them when kExtPlace)
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s);
+// stripes: code kernel + summary scan; then placement scan + pack kernel
+hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s);
+hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s);
+// grids above this many workgroups place by a separate scan (each pack workgroup
+// scanning every record would read G^2 records)
+constexpr uint32_t kInlineScanMaxWgs = 1024;
 
 }  // namespace jpge

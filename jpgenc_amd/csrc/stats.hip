@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         PartView pv;
         pv.load(lds.zz, mask, blk, part, active);
         if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
-            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc));
+            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed));
             atomicAdd(&lds.dcnt[tsel][dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     JPGE_STAMP(2);
 
     const int rep = blockIdx.x % kHistReplicas;
-    const uint64_t ncb = a.g.nmcu();
+    const uint64_t ncb = a.key_ncb ? a.key_ncb : a.g.nmcu();  // Cb blocks of the whole image
 #pragma unroll
     for (int r = 0; r < 1024 / kK2Threads; ++r) {
         const int i = tid + r * kK2Threads;
@@ -124,9 +124,9 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         if (!c) continue;
         atomicAdd(&a.hist.cnt[(rep * 4 + t) * 256 + s], c);
         const uint32_t k32 = lds.key[t][s];
-        uint64_t base;
-        if (t < 2) base = ybase;
-        else base = (k32 & 0x80000000u) ? ncb + cbase : cbase;
+        uint64_t base;  // (global texts: a stripe's bases are offset into the whole image)
+        if (t < 2) base = a.key_y0 + ybase;
+        else base = a.key_c0 + cbase + ((k32 & 0x80000000u) ? ncb : 0ull);
         const uint64_t gkey = (ac ? base * 128ull : base) + (k32 & 0x7FFFFFFFu);
         const unsigned long long inv = ~gkey;
         unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[t * 256 + s]);

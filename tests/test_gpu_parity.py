@@ -101,12 +101,21 @@ def test_batch_matches_single(encoder):
         assert o == _oracle.encode(f, 90)
 
 
-def _encoder_with_wgs(wgs):
-    os.environ["JPGE_ENTROPY_WGS"] = str(wgs)
+def _encoder_with_env(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
     try:
         return J.Encoder(0)
     finally:
-        del os.environ["JPGE_ENTROPY_WGS"]
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _encoder_with_wgs(wgs):
+    return _encoder_with_env(JPGE_ENTROPY_WGS=wgs)
 
 
 # The entropy kernel splits the frame's 128-block tiles into contiguous runs of
@@ -133,6 +142,41 @@ def test_entropy_workgroup_partitions_4k(wgs):
         assert enc.encode(rgb, quality=90) == _oracle.encode(rgb, 90)
     finally:
         enc.close()
+
+
+# Placement by the separate scan kernel (large grids: 16K) must agree with the
+# pack kernel's own scan at every partition.
+@pytest.mark.parametrize("wgs", [1, 5, 100000])
+@pytest.mark.parametrize("w,h,kind,quality", [(500, 300, 1, 100), (1040, 16, 0, 75), (16, 1040, 0, 50),
+                                              (1920, 1080, 0, 90)])
+def test_entropy_scan_kernel_placement(wgs, w, h, kind, quality):
+    enc = _encoder_with_env(JPGE_ENTROPY_WGS=wgs, JPGE_EXT_PLACE=1)
+    try:
+        rgb = J.synth_rgb8(57 + kind + w, w, h, kind=kind)
+        assert enc.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
+    finally:
+        enc.close()
+
+
+def _large_golden(w, h, quality):
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_frames.json")) as f:
+        for fr in json.load(f)["frames"]:
+            if (fr["width"], fr["height"], fr["quality"]) == (w, h, quality):
+                return fr
+    raise KeyError((w, h, quality))
+
+
+# SURVEY 8(d) config 5 on one GPU: 16384x16384 (12288 entropy workgroups, placed by
+# the scan kernel), against the oracle's SHA-256 (tests/golden/make_large.py).
+@pytest.mark.parametrize("quality", [90, 50])
+def test_16k_frame_matches_oracle_hash(encoder, quality):
+    import hashlib
+    g = _large_golden(16384, 16384, quality)
+    rgb = J.synth_rgb8(g["seed"], 16384, 16384, kind=g["kind"])
+    jpg = encoder.encode(rgb, quality=quality)
+    assert len(jpg) == g["len"]
+    assert hashlib.sha256(jpg).hexdigest() == g["sha256"]
 
 
 def test_output_decodes(encoder):
