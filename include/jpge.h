@@ -146,6 +146,48 @@ int jpge_synth_rgb8(uint64_t seed, uint32_t width, uint32_t height, int kind, ui
  * a[0..4] = a1..a5, s[0..7] = s0..s7. */
 void jpge_arai_constants(double a[5], double s[8]);
 
+/* ---- Row stripes of one large image across devices ----
+ * The image (width x height, 4:2:0) is cut into stripes of whole MCU rows (16 px);
+ * each stripe is encoded by its own context (one per GPU) in four phases, with
+ * three small exchanges between them that the caller performs (RCCL all-gather /
+ * all-reduce, or plain copies in one process).  The result is byte-identical to
+ * encoding the whole image at once: the reference never emits restart markers, so
+ * its DC chain (Image.cpp:638-678), its histograms (Image.cpp:888-906) and its
+ * single bit stream (Image.cpp:957-972) run across stripe boundaries.
+ *   1 jpge_stripe_transform  -> last_dc; exchange: all-gather, stripe r's seed = r-1's last_dc
+ *   2 jpge_stripe_stats      -> counts/first; exchange: all-reduce counts (sum), first (min)
+ *   3 jpge_stripe_code       -> summary; exchange: all-gather summaries
+ *   4 jpge_stripe_pack       -> the stripe's bytes at their place in a whole-file device
+ *                               buffer; then gather every [seg_off, seg_off + seg_len) to one rank.
+ * Replaces nothing in the reference (single-process, single-image encoder). */
+typedef struct {
+    uint64_t bits;   /* length of the stripe's bit stream */
+    uint32_t ff[8];  /* 0xFF bytes wholly inside it when it starts at bit a (mod 8) */
+    uint32_t head;   /* its first 8 bits */
+    uint32_t tail;   /* its last 8 bits */
+} jpge_stripe_summary;
+
+/* K1 on MCU rows [mcu_row0, mcu_row0 + mcu_rows) of the image; rgb = device pointer
+ * to the stripe's first pixel row (image row 16*mcu_row0), stride bytes per row. */
+int jpge_stripe_transform(jpge_ctx* ctx, const uint8_t* rgb, size_t stride, uint32_t width, uint32_t height,
+                          uint32_t mcu_row0, uint32_t mcu_rows, int maxval, const uint8_t qy[64],
+                          const uint8_t qc[64], int32_t last_dc[3]);
+/* K2 with the DC chain seeded by the previous stripe's last Y/Cb/Cr DC (0,0,0 for
+ * the first stripe); counts/first as jpge_symbol_stats, keys in the image's texts. */
+int jpge_stripe_stats(jpge_ctx* ctx, const int32_t seed_dc[3], uint32_t counts[1024], uint64_t first[1024]);
+/* Tables from the image's (summed) counts and (minimum) first keys, then the code
+ * kernel; returns the stripe's summary and the header length. */
+int jpge_stripe_code(jpge_ctx* ctx, const uint32_t counts[1024], const uint64_t first[1024],
+                     jpge_stripe_summary* summary, size_t* header_len);
+/* Host only: stripe `index`'s first output byte and the whole file's length. */
+int jpge_stripe_place(const jpge_stripe_summary* all, int n, int index, size_t header_len, size_t* seg_off,
+                      size_t* total_len);
+/* Stuffed bytes of stripe `index` into out (device, whole-file capacity cap) at
+ * [seg_off, seg_off + seg_len); stripe 0 includes the headers, the last one the
+ * 1-fill and EOI. */
+int jpge_stripe_pack(jpge_ctx* ctx, const jpge_stripe_summary* all, int n, int index, uint8_t* out, size_t cap,
+                     size_t* seg_off, size_t* seg_len, size_t* total_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,7 @@ EXPORTS = (
     "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_synth_rgb8", "jpge_arai_constants",
+    "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
 )
 
 
@@ -50,6 +51,24 @@ class Frame(ctypes.Structure):
         ("stride", ctypes.c_size_t), ("maxval", ctypes.c_int), ("out", ctypes.c_void_p),
         ("cap", ctypes.c_size_t), ("len", ctypes.c_size_t), ("status", ctypes.c_int),
     ]
+
+
+class StripeSummary(ctypes.Structure):
+    """jpge_stripe_summary: a stripe's bit count, inside-0xFF count per start
+    alignment, first and last 8 bits."""
+    _fields_ = [("bits", ctypes.c_uint64), ("ff", ctypes.c_uint32 * 8), ("head", ctypes.c_uint32),
+                ("tail", ctypes.c_uint32)]
+
+    def as_tuple(self):
+        return (int(self.bits), tuple(int(x) for x in self.ff), int(self.head), int(self.tail))
+
+    @classmethod
+    def from_tuple(cls, t):
+        s = cls()
+        s.bits, s.head, s.tail = t[0], t[2], t[3]
+        for i in range(8):
+            s.ff[i] = t[1][i]
+        return s
 
 
 class Timing(ctypes.Structure):
@@ -86,6 +105,13 @@ def lib() -> ctypes.CDLL:
         L.jpge_encode_batch.argtypes = [vp, ctypes.POINTER(Frame), i32, vp, vp, u32]
         L.jpge_fdct_quant.argtypes = [vp, vp, u32, u32, sz, i32, vp, vp, vp, vp, vp, u32]
         L.jpge_symbol_stats.argtypes = [vp, vp, u32, u32, sz, i32, vp, vp, vp, vp, u32]
+        L.jpge_stripe_transform.argtypes = [vp, vp, sz, u32, u32, u32, u32, i32, vp, vp, vp]
+        L.jpge_stripe_stats.argtypes = [vp, vp, vp, vp]
+        L.jpge_stripe_code.argtypes = [vp, vp, vp, ctypes.POINTER(StripeSummary), ctypes.POINTER(sz)]
+        L.jpge_stripe_place.argtypes = [ctypes.POINTER(StripeSummary), i32, i32, sz, ctypes.POINTER(sz),
+                                        ctypes.POINTER(sz)]
+        L.jpge_stripe_pack.argtypes = [vp, ctypes.POINTER(StripeSummary), i32, i32, vp, sz, ctypes.POINTER(sz),
+                                       ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.jpge_huffman_table.argtypes = [vp, vp, vp, vp, ctypes.POINTER(i32), vp, vp]
         L.jpge_huffman_text.argtypes = [vp, sz, vp, vp, vp, ctypes.POINTER(i32)]
         L.jpge_parse_ppm.argtypes = [vp, sz, vp, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
@@ -314,6 +340,39 @@ class Encoder:
                                      _p(cr), 0), "fdct_quant")
         return y, cb, cr
 
+    # ---- row stripes (jpge_stripe_*; orchestration in jpgenc_amd.stripes) ----
+    def stripe_transform(self, rgb_ptr: int, stride: int, width: int, height: int, mcu_row0: int, mcu_rows: int,
+                         quality: int = 50, maxval: int = 255) -> np.ndarray:
+        """K1 on a stripe (device RGB of its rows); returns its last Y/Cb/Cr DC (int32[3])."""
+        qy, qc = self._tables(quality, None, None)
+        last = np.zeros(3, np.int32)
+        _check(lib().jpge_stripe_transform(self._ctx, rgb_ptr, stride, width, height, mcu_row0, mcu_rows,
+                                           int(maxval), _p(qy), _p(qc), _p(last)), "stripe_transform")
+        return last
+
+    def stripe_stats(self, seed_dc) -> tuple[np.ndarray, np.ndarray]:
+        seed = np.ascontiguousarray(seed_dc, np.int32)
+        counts = np.zeros(1024, np.uint32)
+        first = np.zeros(1024, np.uint64)
+        _check(lib().jpge_stripe_stats(self._ctx, _p(seed), _p(counts), _p(first)), "stripe_stats")
+        return counts, first
+
+    def stripe_code(self, counts: np.ndarray, first: np.ndarray) -> tuple[tuple, int]:
+        counts = np.ascontiguousarray(counts, np.uint32)
+        first = np.ascontiguousarray(first, np.uint64)
+        sm = StripeSummary()
+        hl = ctypes.c_size_t()
+        _check(lib().jpge_stripe_code(self._ctx, _p(counts), _p(first), ctypes.byref(sm), ctypes.byref(hl)),
+               "stripe_code")
+        return sm.as_tuple(), hl.value
+
+    def stripe_pack(self, summaries: list, index: int, out_ptr: int, cap: int) -> tuple[int, int, int]:
+        arr = (StripeSummary * len(summaries))(*[StripeSummary.from_tuple(t) for t in summaries])
+        off, ln, tot = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib().jpge_stripe_pack(self._ctx, arr, len(summaries), index, out_ptr, cap, ctypes.byref(off),
+                                      ctypes.byref(ln), ctypes.byref(tot)), "stripe_pack")
+        return off.value, ln.value, tot.value
+
     def symbol_stats(self, rgb: np.ndarray, quality: int = 50, maxval: int = 255):
         rgb = np.ascontiguousarray(rgb, np.uint8)
         h, w = rgb.shape[:2]
@@ -323,6 +382,15 @@ class Encoder:
         _check(lib().jpge_symbol_stats(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(counts),
                                        _p(first), 0), "symbol_stats")
         return counts.reshape(4, 256), first.reshape(4, 256)
+
+
+def stripe_place(summaries: list, index: int, header_len: int) -> tuple[int, int]:
+    """Host-only placement of stripe `index`: (first output byte, whole file length)."""
+    arr = (StripeSummary * len(summaries))(*[StripeSummary.from_tuple(t) for t in summaries])
+    off, tot = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(lib().jpge_stripe_place(arr, len(summaries), index, header_len, ctypes.byref(off), ctypes.byref(tot)),
+           "stripe_place")
+    return off.value, tot.value
 
 
 def write_jpeg(path: str, ppm: PPM, quality: int = 50, device: int = 0) -> int:

@@ -240,4 +240,45 @@ void jpge_arai_constants(double a[5], double s[8]) {
     s[4] = jpge::kS4; s[5] = jpge::kS5; s[6] = jpge::kS6; s[7] = jpge::kS7;
 }
 
+static_assert(sizeof(jpge_stripe_summary) == sizeof(jpge::StripeSummary), "stripe summary layout");
+
+int jpge_stripe_transform(jpge_ctx* ctx, const uint8_t* rgb, size_t stride, uint32_t width, uint32_t height,
+                          uint32_t mcu_row0, uint32_t mcu_rows, int maxval, const uint8_t qy[64],
+                          const uint8_t qc[64], int32_t last_dc[3]) {
+    if (!ctx || !rgb || !qy || !qc || !last_dc) return JPGE_E_ARG;
+    jpge::Encoder::StripeDesc d;
+    d.rgb = rgb;
+    d.stride = stride;
+    d.width = width;
+    d.height = height;
+    d.mcu_row0 = mcu_row0;
+    d.mcu_rows = mcu_rows;
+    d.maxval = maxval;
+    return ctx->enc->stripe_transform(d, qy, qc, last_dc);
+}
+
+int jpge_stripe_stats(jpge_ctx* ctx, const int32_t seed_dc[3], uint32_t counts[1024], uint64_t first[1024]) {
+    if (!ctx || !seed_dc || !counts || !first) return JPGE_E_ARG;
+    return ctx->enc->stripe_stats(seed_dc, counts, first);
+}
+
+int jpge_stripe_code(jpge_ctx* ctx, const uint32_t counts[1024], const uint64_t first[1024],
+                     jpge_stripe_summary* summary, size_t* header_len) {
+    if (!ctx || !counts || !first || !summary) return JPGE_E_ARG;
+    return ctx->enc->stripe_code(counts, first, reinterpret_cast<jpge::StripeSummary*>(summary), header_len);
+}
+
+int jpge_stripe_place(const jpge_stripe_summary* all, int n, int index, size_t header_len, size_t* seg_off,
+                      size_t* total_len) {
+    return jpge::Encoder::stripe_place(reinterpret_cast<const jpge::StripeSummary*>(all), n, index, header_len,
+                                       nullptr, nullptr, nullptr, seg_off, total_len);
+}
+
+int jpge_stripe_pack(jpge_ctx* ctx, const jpge_stripe_summary* all, int n, int index, uint8_t* out, size_t cap,
+                     size_t* seg_off, size_t* seg_len, size_t* total_len) {
+    if (!ctx || !all || !out) return JPGE_E_ARG;
+    return ctx->enc->stripe_pack(reinterpret_cast<const jpge::StripeSummary*>(all), n, index, out, cap, seg_off,
+                                 seg_len, total_len);
+}
+
 }  // extern "C"

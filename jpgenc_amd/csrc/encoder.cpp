@@ -219,6 +219,11 @@ struct Encoder::Slot {
     std::atomic<int> tables_done{0};   // set by build_tables (any thread)
     std::atomic<int> export_queued{0}; // the kernel exporting this frame's histograms is launched
     std::chrono::steady_clock::time_point t_submit, t_start, t_done;  // table job (host trace)
+    // stripe context (a row stripe of a larger image; whole frames: zero seeds and
+    // bases, header dimensions = the frame's)
+    DcSeed seed;
+    uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
+    uint32_t img_w = 0, img_h = 0;
     int tables_status = 0;
 
     ~Slot() {
@@ -415,6 +420,71 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     return kOk;
 }
 
+// Kernel parameter blocks of a slot's frame (or stripe).
+FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
+    const CtlLayout L(entropy_tiles(s.g));
+    FdctArgs a;
+    a.rgb = s.in_dev;
+    a.stride = s.in_stride;
+    a.g = s.g;
+    a.maxval = maxval;
+    for (int i = 0; i < 64; ++i) {
+        a.q[i] = s.qy[i];
+        a.q[64 + i] = s.qc[i];
+    }
+    a.coef = s.d_coef;
+    a.zero = reinterpret_cast<uint32_t*>(s.d_ctl);
+    a.zero_words = (uint32_t)(L.total / 4);
+    a.imp_src = imp ? reinterpret_cast<const uint4*>(imp->d_tab_host) : nullptr;
+    a.imp_dst = imp ? reinterpret_cast<uint4*>(imp->d_tab) : nullptr;
+    a.imp_n16 = imp ? (uint32_t)((kTabBytes + imp->hdr_len + 15) / 16) : 0u;
+    a.dbg = d_dbg_;
+    return a;
+}
+
+StatsArgs Encoder::stats_args(Slot& s) {
+    const CtlLayout L(entropy_tiles(s.g));
+    StatsArgs st;
+    st.coef = s.d_coef;
+    st.g = s.g;
+    st.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
+    st.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
+    st.seed = s.seed;
+    st.key_y0 = s.key_y0;
+    st.key_c0 = s.key_c0;
+    st.key_ncb = s.key_ncb;
+    st.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
+    return st;
+}
+
+EntropyArgs Encoder::entropy_args(Slot& s) {
+    const CtlLayout L(entropy_tiles(s.g));
+    EntropyArgs e;
+    e.coef = s.d_coef;
+    e.g = s.g;
+    e.tables = s.d_tab;
+    e.out = s.out_dev;
+    e.hdr_len = s.hdr_len;
+    e.out_cap = s.out_cap;
+    e.rec = s.d_ctl + L.rec;
+    e.place = reinterpret_cast<WgPlace*>(s.d_ctl + L.place);
+    e.summary = reinterpret_cast<StripeSummary*>(s.d_ctl + L.summary);
+    if (ext_place_) e.flags |= kExtPlace;
+    e.host_result = s.d_result_host;
+    e.seq = s.seq;
+    e.ubuf = s.d_ubuf;
+    e.wgs = entropy_wgs_;
+    e.diag = diag_;
+    e.seed = s.seed;
+    e.exp_hist = HistPtrs{};
+    e.exp_cnt = nullptr;
+    e.exp_key = nullptr;
+    e.exp_seq = nullptr;
+    e.exp_seqv = 0;
+    e.dbg = d_dbg_ ? d_dbg_ + 2 * 65536 * kStampSlots : nullptr;
+    return e;
+}
+
 // Phase 1: upload (if host input), statistics kernels, histogram read-back.
 int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                     Slot* imp, bool export_hist) {
@@ -449,30 +519,12 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         s.out_dev = s.d_out;
         s.out_cap = s.cap_out;
     }
-    const CtlLayout L(entropy_tiles(g));
-
-    FdctArgs a;
-    a.rgb = s.in_dev;
-    a.stride = s.in_stride;
-    a.g = g;
-    a.maxval = f.maxval;
-    for (int i = 0; i < 64; ++i) {
-        a.q[i] = qy[i];
-        a.q[64 + i] = qc[i];
-    }
-    a.coef = s.d_coef;
-    a.zero = reinterpret_cast<uint32_t*>(s.d_ctl);
-    a.zero_words = (uint32_t)(L.total / 4);
-    a.imp_src = imp ? reinterpret_cast<const uint4*>(imp->d_tab_host) : nullptr;
-    a.imp_dst = imp ? reinterpret_cast<uint4*>(imp->d_tab) : nullptr;
-    a.imp_n16 = imp ? (uint32_t)((kTabBytes + imp->hdr_len + 15) / 16) : 0u;
-    a.dbg = d_dbg_;
-    StatsArgs st2;
-    st2.coef = s.d_coef;
-    st2.g = g;
-    st2.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
-    st2.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
-    st2.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
+    s.seed = DcSeed();
+    s.key_y0 = s.key_c0 = s.key_ncb = 0;
+    s.img_w = f.width;
+    s.img_h = f.height;
+    const FdctArgs a = fdct_args(s, f.maxval, imp);
+    const StatsArgs st2 = stats_args(s);
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
     s.tables_done.store(0, std::memory_order_relaxed);
     s.export_queued.store(0, std::memory_order_relaxed);
@@ -497,17 +549,23 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel) {
     if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, /*nap=*/!parallel, &s.export_queued)) return w;
+    uint32_t cnt[1024];
+    uint64_t first[1024];
+    for (int i = 0; i < 1024; ++i) {
+        cnt[i] = s.h_hist->cnt[i];
+        first[i] = ~s.h_hist->key[i];
+    }
+    return build_tables_from(s, cnt, first, parallel);
+}
+
+// The four tables from counts and first-occurrence keys, and the headers (the
+// image's real dimensions in SOF0), into the slot's pinned staging buffer.
+int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t* first_all, bool parallel) {
     HuffTable tabs[4];
     int ok[4] = {0, 0, 0, 0};
     // the four tables are independent; the AC tables dominate
     parallel_for(4, parallel ? 4 : 1, [&](long t) {
-        uint32_t cnt[256];
-        uint64_t first[256];
-        for (int i = 0; i < 256; ++i) {
-            cnt[i] = s.h_hist->cnt[t * 256 + i];
-            first[i] = ~s.h_hist->key[t * 256 + i];
-        }
-        if (!build_table(cnt, first, tabs[t])) return;
+        if (!build_table(cnt_all + t * 256, first_all + t * 256, tabs[t])) return;
         for (int i = 0; i < 256; ++i)
             s.h_tab[t * 256 + i] = ((uint32_t)tabs[t].len[i] << 16) | (tabs[t].code[i] & 0xFFFF);
         ok[t] = 1;
@@ -515,11 +573,11 @@ int Encoder::build_tables(Slot& s, bool parallel) {
     const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
     if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
-    const std::vector<uint8_t> hdr = jfif_headers(s.g.width, s.g.height, s.qy, s.qc, tp);
+    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp);
     if (hdr.size() > kHdrMax) return kErrInternal;
     std::memcpy(reinterpret_cast<uint8_t*>(s.h_tab) + kTabBytes, hdr.data(), hdr.size());
     s.hdr_len = hdr.size();
-    if (s.out_cap < s.hdr_len + 2) return kErrNoSpace;
+    if (s.out_cap && s.out_cap < s.hdr_len + 2) return kErrNoSpace;
     return kOk;
 }
 
@@ -532,29 +590,13 @@ int Encoder::import_tables_copy(Slot& s) {
 // Phase 2b (GPU): the entropy kernels (tables already on the device); `exp`: a
 // later frame whose histograms the code kernel exports on the way.
 int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
-    const CtlLayout L(entropy_tiles(s.g));
-    EntropyArgs e;
-    e.coef = s.d_coef;
-    e.g = s.g;
-    e.tables = s.d_tab;
-    e.out = s.out_dev;
-    e.hdr_len = s.hdr_len;
-    e.out_cap = s.out_cap;
-    e.rec = s.d_ctl + L.rec;
-    e.place = reinterpret_cast<WgPlace*>(s.d_ctl + L.place);
-    if (ext_place_) e.flags |= kExtPlace;
-    e.host_result = s.d_result_host;
-    e.seq = s.seq;
+    EntropyArgs e = entropy_args(s);
     s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1)
-    e.ubuf = s.d_ubuf;
-    e.wgs = entropy_wgs_;
-    e.diag = diag_;
     e.exp_hist = exp ? exp->hist : HistPtrs{};
     e.exp_cnt = exp ? exp->d_hist_host->cnt : nullptr;
     e.exp_key = exp ? exp->d_hist_host->key : nullptr;
     e.exp_seq = exp ? &exp->d_hist_host->seq : nullptr;
     e.exp_seqv = exp ? exp->seq : 0;
-    e.dbg = d_dbg_ ? d_dbg_ + 2 * 65536 * kStampSlots : nullptr;
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
     JPGE_HIP(launch_entropy(e, s.stream));
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[5], s.stream));
@@ -822,6 +864,147 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
             first[t * 256 + i] = c ? ~s.h_hist->key[t * 256 + i] : ~0ull;
         }
     return kOk;
+}
+
+
+// ---- stripes ----
+// A stripe is the MCU rows [mcu_row0, mcu_row0 + mcu_rows) of a width x height
+// image; its own geometry has the stripe's real pixel rows (the last stripe's bottom
+// padding replicates the image's last row, Image.cpp:511-519).  Every phase runs on
+// lane 0's first slot and returns when its results are on the host.
+int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]) {
+    JPGE_HIP(hipSetDevice(device_));
+    if (!d.rgb || !last_dc || d.width == 0 || d.height == 0 || d.width > 65535 || d.height > 65535) return kErrArg;
+    if (d.maxval < 1 || d.maxval > 255) return kErrRange;
+    const uint32_t mh_img = (d.height + 15) / 16;
+    if (d.mcu_rows == 0 || d.mcu_row0 >= mh_img || d.mcu_rows > mh_img - d.mcu_row0) return kErrArg;
+    const size_t row = (size_t)d.width * 3, stride = d.stride ? d.stride : row;
+    if (stride < row) return kErrArg;
+    for (int i = 0; i < 64; ++i)
+        if (!qy[i] || !qc[i]) return kErrArg;
+    const uint32_t hs = std::min(16 * d.mcu_rows, d.height - 16 * d.mcu_row0);
+    const Geometry g = geometry(d.width, hs);
+    Slot& s = *lanes_[0]->slots[0];
+    if (const int st = ensure(s, g, 0, 0)) return st;
+    std::memcpy(s.qy, qy, 64);
+    std::memcpy(s.qc, qc, 64);
+    s.g = g;
+    s.in_dev = d.rgb;
+    s.in_stride = stride;
+    s.img_w = d.width;
+    s.img_h = d.height;
+    s.seed = DcSeed();
+    s.key_y0 = 2ull * d.mcu_row0 * (2ull * g.mw);  // Y blocks above the stripe (raster)
+    s.key_c0 = (uint64_t)d.mcu_row0 * g.mw;         // Cb blocks above it
+    s.key_ncb = (uint64_t)mh_img * g.mw;            // Cb blocks of the image
+    JPGE_HIP(launch_fdct(fdct_args(s, d.maxval, nullptr), s.stream));
+    int16_t lastmcu[6 * 64];  // the stripe's last MCU: its Y11, Cb and Cr DCs seed the next stripe
+    JPGE_HIP(hipMemcpyAsync(lastmcu, s.d_coef + ((size_t)g.nmcu() - 1) * 384, sizeof lastmcu, hipMemcpyDeviceToHost,
+                            s.stream));
+    JPGE_HIP(hipStreamSynchronize(s.stream));
+    last_dc[0] = lastmcu[3 * 64];
+    last_dc[1] = lastmcu[4 * 64];
+    last_dc[2] = lastmcu[5 * 64];
+    return kOk;
+}
+
+int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t first[1024]) {
+    JPGE_HIP(hipSetDevice(device_));
+    Slot& s = *lanes_[0]->slots[0];
+    if (!s.in_dev || !seed || !counts || !first) return kErrArg;
+    for (int c = 0; c < 3; ++c) s.seed.v[c] = seed[c];
+    const StatsArgs st = stats_args(s);
+    JPGE_HIP(launch_stats(st, s.stream));
+    s.seq = ++seq_counter_;
+    s.hist = st.hist;
+    JPGE_HIP(launch_hist_export(st.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq, s.stream));
+    JPGE_HIP(hipStreamSynchronize(s.stream));
+    for (int i = 0; i < 1024; ++i) {
+        const uint32_t c = s.h_hist->cnt[i];
+        counts[i] = c;
+        first[i] = c ? ~s.h_hist->key[i] : ~0ull;
+    }
+    return kOk;
+}
+
+int Encoder::stripe_code(const uint32_t counts[1024], const uint64_t first[1024], StripeSummary* sum,
+                         size_t* hdr_len) {
+    JPGE_HIP(hipSetDevice(device_));
+    Slot& s = *lanes_[0]->slots[0];
+    if (!s.in_dev || !counts || !first || !sum) return kErrArg;
+    s.out_dev = nullptr;
+    s.out_cap = 0;
+    if (const int st = build_tables_from(s, counts, first, true)) return st;
+    if (const int st = import_tables_copy(s)) return st;
+    EntropyArgs e = entropy_args(s);
+    JPGE_HIP(launch_entropy_code_summary(e, s.stream));
+    JPGE_HIP(hipMemcpyAsync(sum, e.summary, sizeof(StripeSummary), hipMemcpyDeviceToHost, s.stream));
+    JPGE_HIP(hipStreamSynchronize(s.stream));
+    if (hdr_len) *hdr_len = s.hdr_len;
+    return kOk;
+}
+
+namespace {
+uint32_t split_bits(uint32_t ptail, uint32_t head, uint32_t b) {  // 0 < b < 8 (entropy.hip)
+    return (((ptail & ((1u << b) - 1)) << (8 - b)) | ((head & 0xFF) >> b)) & 0xFF;
+}
+uint32_t fill_bits(uint32_t eb, uint32_t tail) {  // Bitstream::fill, BitstreamGeneric.hpp:243-248
+    return (((tail & ((1u << eb) - 1)) << (8 - eb)) | (0xFFu >> eb)) & 0xFF;
+}
+}  // namespace
+
+int Encoder::stripe_place(const StripeSummary* all, int n, int index, size_t hdr_len, uint64_t* p_ext,
+                          uint64_t* q_ext, uint32_t* head_split, size_t* seg_off, size_t* total_len) {
+    if (!all || n <= 0 || index < 0 || index >= n) return kErrArg;
+    uint64_t p = 0, q = 0;
+    for (int r = 0; r < n; ++r) {
+        if (all[r].bits < 8) return kErrArg;  // (a stripe codes >= 2 bits per block, 6 blocks per MCU)
+        const uint32_t b = (uint32_t)(p & 7);
+        const uint32_t split = (b && r > 0) ? split_bits(all[r - 1].tail, all[r].head, b) : 0u;
+        if (r == index) {
+            if (p_ext) *p_ext = p;
+            if (q_ext) *q_ext = q;
+            if (head_split) *head_split = split;
+            if (seg_off) *seg_off = r == 0 ? 0 : hdr_len + (size_t)(p >> 3) + (size_t)q;
+        }
+        // 0xFF bytes stripe r owns: its inside bytes at its alignment, the byte it
+        // shares with its predecessor, the image's 1-filled final byte
+        q += all[r].ff[b] + ((b && r > 0 && split == 0xFF) ? 1u : 0u);
+        p += all[r].bits;
+        if (r == n - 1 && (p & 7) && fill_bits((uint32_t)(p & 7), all[r].tail) == 0xFF) q += 1;
+    }
+    if (total_len) *total_len = hdr_len + (size_t)((p + 7) >> 3) + (size_t)q + 2;
+    return kOk;
+}
+
+int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* out_dev, size_t cap, size_t* seg_off,
+                         size_t* seg_len, size_t* total_len) {
+    JPGE_HIP(hipSetDevice(device_));
+    Slot& s = *lanes_[0]->slots[0];
+    if (!s.in_dev || !out_dev || !s.hdr_len) return kErrArg;
+    uint64_t p_ext = 0, q_ext = 0;
+    uint32_t head = 0;
+    size_t off = 0, total = 0;
+    if (const int st = stripe_place(all, n, index, s.hdr_len, &p_ext, &q_ext, &head, &off, &total)) return st;
+    if (total > cap) return kErrNoSpace;
+    s.out_dev = out_dev;
+    s.out_cap = cap;
+    s.seq = ++seq_counter_;
+    s.h_result[2] = 0;
+    EntropyArgs e = entropy_args(s);
+    e.p_ext = p_ext;
+    e.q_ext = q_ext;
+    e.head_split = head;
+    e.flags = (index == 0 ? kStripeFirst : 0u) | (index == n - 1 ? kStripeLast : 0u) | kExtPlace;
+    JPGE_HIP(launch_entropy_place_pack(e, s.stream));
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream)) return w;
+    JPGE_HIP(hipStreamSynchronize(s.stream));
+    if (s.h_result[1] & 4) return kErrNoSpace;
+    const size_t end = (size_t)s.h_result[0];
+    if (seg_off) *seg_off = off;
+    if (seg_len) *seg_len = end - off;
+    if (total_len) *total_len = total;
+    return (index == n - 1 && end != total) ? kErrInternal : kOk;
 }
 
 }  // namespace jpge

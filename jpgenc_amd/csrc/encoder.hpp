@@ -56,6 +56,28 @@ class Encoder {
     int symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                      uint32_t counts[1024], uint64_t first[1024]);
 
+    // ---- row stripes of a larger image (one stripe per device) ----
+    // Phases, with the exchanges between them done by the caller (RCCL or a test):
+    //   transform -> all-gather last DCs -> stats(seed = previous stripe's last DCs)
+    //   -> all-reduce counts (sum) / keys (min) -> code -> all-gather summaries -> pack.
+    struct StripeDesc {
+        const uint8_t* rgb = nullptr;  // device: first pixel row of the stripe (row 16*mcu_row0)
+        size_t stride = 0;
+        uint32_t width = 0, height = 0;   // whole image
+        uint32_t mcu_row0 = 0, mcu_rows = 0;
+        int maxval = 255;
+    };
+    int stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]);
+    int stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t first[1024]);
+    int stripe_code(const uint32_t counts[1024], const uint64_t first[1024], StripeSummary* sum, size_t* hdr_len);
+    int stripe_pack(const StripeSummary* all, int n, int index, uint8_t* out_dev, size_t cap, size_t* seg_off,
+                    size_t* seg_len, size_t* total_len);
+    // Host arithmetic: where stripe `index` starts (global bit p_ext, stuffing bytes
+    // q_ext before it, the byte it shares with its predecessor), its first output
+    // byte and the whole file's length.
+    static int stripe_place(const StripeSummary* all, int n, int index, size_t hdr_len, uint64_t* p_ext,
+                            uint64_t* q_ext, uint32_t* head_split, size_t* seg_off, size_t* total_len);
+
     // Kernel timing with HIP events: 0 off, N >= 1 brackets the kernels of every
     // N-th frame (events cost GPU time; sampling keeps the pipeline's shape).
     void set_timing(int every) { timing_every_ = every > 0 ? every : 0; }
@@ -78,6 +100,10 @@ class Encoder {
                bool export_hist);
     // phase 2a (host, any thread): Huffman tables + headers from the histograms
     int build_tables(Slot& s, bool parallel);
+    int build_tables_from(Slot& s, const uint32_t* cnt, const uint64_t* first, bool parallel);
+    FdctArgs fdct_args(Slot& s, int maxval, Slot* imp);
+    StatsArgs stats_args(Slot& s);
+    EntropyArgs entropy_args(Slot& s);
     // phase 2b (GPU): table upload (when not carried) + entropy kernels
     int import_tables_copy(Slot& s);
     int launch_entropy_phase(Slot& s, Slot* exp);
