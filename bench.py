@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--solo-batches", type=int, default=2,
                     help="batches through a 1-lane encoder after the timed region (kernel times alone; 0 = skip)")
     ap.add_argument("--lanes", type=int, default=0, help="encoder lanes (0 = library default)")
+    ap.add_argument("--workload", choices=["4k-frames", "16k-striped"], default="4k-frames",
+                    help="4k-frames: the BASELINE metric (frames sharded over ranks); 16k-striped: one "
+                         "16384x16384 frame per step, row-striped over the ranks (SURVEY 8(e) config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
@@ -167,9 +170,73 @@ def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
     return {}
 
 
+def run_striped16k(args, rank, local, world, pg):
+    """One 16384^2 frame per step: whole-frame encode on one GPU; on N GPUs each
+    rank holds and encodes its row stripe, with the three RCCL exchanges and the
+    segment gather of SURVEY 8(e) inside the timed step (output identical to 1 GPU)."""
+    import torch
+
+    import jpgenc_amd as J
+    from jpgenc_amd import stripes
+
+    torch.cuda.set_device(local)
+    W = H = 16384
+    rgb = J.synth_rgb8(5, W, H)  # SURVEY 8(d) config 5 seed
+    cap = J.max_jpeg_bytes(W, H)
+    out = torch.empty(cap, dtype=torch.uint8, device=f"cuda:{local}")
+    if world == 1:
+        enc = J.Encoder(local)
+        src = torch.from_numpy(rgb.reshape(-1)).to(f"cuda:{local}")
+        del rgb
+
+        def step():
+            return enc.encode_batch_dev([(src.data_ptr(), W, H, W * 3)], [(out.data_ptr(), cap)],
+                                        quality=args.quality)[0]
+    else:
+        import torch.distributed as dist
+
+        rccl = dist.new_group(backend="nccl")  # the exchanges and the gather ride RCCL over xGMI
+        r0, nr = stripes.stripe_rows(H // 16, world)[rank]
+        src = torch.from_numpy(np.ascontiguousarray(rgb[16 * r0:16 * (r0 + nr)]).reshape(-1)).to(f"cuda:{local}")
+        del rgb
+        enc = J.Encoder(local, lanes=1)
+
+        def step():
+            return stripes.encode_stripe_dist(enc, src.data_ptr(), W * 3, W, H, args.quality, out, group=rccl)
+    for _ in range(args.warmup):
+        n = step()
+    torch.cuda.synchronize()
+    barrier(pg)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n = step()
+    torch.cuda.synchronize()
+    barrier(pg)
+    dt = max_over_ranks(pg, time.perf_counter() - t0)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "MPixels/s encode (16K 4:2:0 Q=90)",
+            "value": round(W * H * args.steps / dt / 1e6, 1), "unit": "MPix/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (deterministic splitmix64 photo-like frame, seed 5, HBM-resident)",
+            "config": {"workload": f"16384x16384 4:2:0 Q{args.quality}, one frame per step, "
+                                   + ("whole frame on one GPU" if world == 1 else
+                                      f"row-striped over {world} GPUs (RCCL: DC seeds, histogram sum/min, "
+                                      f"summaries; segments gathered to rank 0)"),
+                       "jpeg_bytes": int(n)},
+        }), flush=True)
+    enc.close()
+
+
 def main():
     args = parse()
     rank, local, world, pg = dist_setup(args.gpus)
+    if args.workload == "16k-striped":
+        run_striped16k(args, rank, local, world, pg)
+        if pg is not None:
+            pg.destroy_process_group()
+        return
     import torch
 
     import jpgenc_amd as J
