@@ -159,15 +159,21 @@ def thread_cpu() -> dict:
 
 
 def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
-    """Per-launch HBM bytes per kernel from the committed rocprofv3 PMC summary."""
+    """Per-launch HBM bytes per stage from the committed rocprofv3 PMC summary (the
+    entropy stage = its code, placement-scan and pack kernels)."""
     try:
         with open(os.path.join(profile_dir, "pmc_r01.json")) as f:
             d = json.load(f)
-        if d.get("width") == width and d.get("height") == height:
-            return {k.split("<")[0]: v["hbm_bytes_per_launch"] for k, v in d["kernels"].items()}
+        if d.get("width") != width or d.get("height") != height:
+            return {}
+        per = {k.split("<")[0]: v["hbm_bytes_per_launch"] for k, v in d["kernels"].items()}
     except (OSError, ValueError, KeyError):
-        pass
-    return {}
+        return {}
+    out = {k: v for k, v in per.items() if not k.startswith("entropy_")}
+    ent = [v for k, v in per.items() if k.startswith("entropy_")]
+    if ent:
+        out["entropy_kernel"] = sum(ent)
+    return out
 
 
 def run_striped16k(args, rank, local, world, pg):
@@ -272,6 +278,7 @@ def main():
     barrier(pg)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    win0 = time.monotonic_ns()
     total_bytes = 0
     step_t = []
     cg0 = cgroup_cpu_stat()
@@ -284,6 +291,7 @@ def main():
     torch.cuda.synchronize()
     barrier(pg)
     dt = time.perf_counter() - t0
+    win1 = time.monotonic_ns()
     cg1 = cgroup_cpu_stat()
     if th0:
         th1 = thread_cpu()
@@ -303,13 +311,16 @@ def main():
     # a single-lane encoder with events around every frame's kernels, so each kernel's
     # duration is its own, without other lanes' kernels beside it.
     tm_solo = None
+    solo_win = None
     if args.solo_batches > 0 and not args.no_kernel_events:
         solo = J.Encoder(local, lanes=1)
         solo.encode_batch_dev(frames, outd, quality=args.quality)
         solo.set_timing(1)
         solo.reset_timing()
+        s0 = time.monotonic_ns()
         for _ in range(args.solo_batches):
             solo.encode_batch_dev(frames, outd, quality=args.quality)
+        solo_win = [s0, time.monotonic_ns()]
         tm_solo = solo.timing()
         solo.close()
 
@@ -382,6 +393,8 @@ def main():
             "step_ms": {"min": round(min(step_t) * 1e3, 3), "median": round(sorted(step_t)[len(step_t) // 2] * 1e3, 3),
                         "max": round(max(step_t) * 1e3, 3)},
             "lanes": enc.lanes(),
+            # CLOCK_MONOTONIC windows (rocprofv3 timestamps use the same clock): tools/rocprof_window.py
+            "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win},
             # host CPU use over the timed region; quota throttling stalls the pipeline
             "host_cpu": {"cpus_used": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e6 / dt, 2),
                          "throttled_periods": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
