@@ -53,6 +53,13 @@ __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 }
+// The same ordering without the wait: a wave's DS instructions execute in issue
+// order, so a read issued after another lane's write sees it; only the compiler
+// must not move LDS accesses across this point.
+__device__ __forceinline__ void wave_order() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
 
 // getCategoryAndCode, Coding.hpp:197-230: bit length of |v| (0 for v == 0)
 __device__ __forceinline__ int category(int v) {

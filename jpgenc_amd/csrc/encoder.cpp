@@ -377,7 +377,7 @@ void Encoder::dump_stamps(const Slot& s) {
     if (!stamps_file_ || !d_dbg_) return;
     std::vector<uint64_t> h(dbg_words_);
     if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const uint64_t hdr[4] = {fdct_grid(s.g), stats_grid(s.g), entropy_grid(s.g, entropy_wgs_),
+    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(s.g), entropy_grid(s.g, entropy_wgs_),
                              entropy_grid(s.g, entropy_wgs_)};
     FILE* f = std::fopen(stamps_file_, "wb");
     if (!f) return;
@@ -428,6 +428,7 @@ FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
     a.stride = s.in_stride;
     a.g = s.g;
     a.maxval = maxval;
+    a.solo = lanes_.size() == 1;  // (several lanes: K1 runs beside other frames' kernels)
     for (int i = 0; i < 64; ++i) {
         a.q[i] = s.qy[i];
         a.q[64 + i] = s.qc[i];

@@ -3,8 +3,15 @@
 //
 // One wavefront owns a tile of 4 MCUs (64x16 px) staged in LDS for the column
 // pass, the transpose and the row pass; each lane stores one 16-byte row of a
-// block straight from registers.  Persistent grid: a wave walks tiles with a
-// stride of all waves, prefetching its next tile's RGB run during the transform.
+// block straight from registers.  One persistent 16-wave workgroup per CU owns a
+// contiguous run of tiles; its waves take tiles from an LDS counter (the SIMD
+// favours its oldest wave, so static shares finish unevenly) and prefetch the next
+// tile's RGB run during the transform.  Three rounds per tile (chroma, Y MCUs 0-1,
+// Y MCUs 2-3), each round's LDS reads issued in one batch during the previous
+// round's row pass.  Pixels and coefficients go through buffer descriptors so that
+// every tile issues the same loads and stores (no branches around them) and the
+// in-order wait for the prefetch never drains a just-issued store; the stores are
+// write-through (sc1), so the kernel ends without dirty L2 lines to flush.
 // Reference: Image.cpp:112-147, 198-235, 540-636; Dct.hpp:47-215; Coding.hpp:84-97.
 //
 // Bit-exactness: every fp64 operation of the reference is reproduced in order with
@@ -23,8 +30,9 @@ constexpr double kYr = (double).299f, kYg = (double).587f, kYb = (double).114f;
 constexpr double kCbR = (double)-.1687f, kCbG = (double)-.3312f, kCbB = (double).5f;
 constexpr double kCrR = (double).5f, kCrG = (double)-.4186f, kCrB = (double)-.0813f;
 
-// One 8-point Arai pass, Dct.hpp:62-131 (same op order for both passes).
-__device__ __forceinline__ void arai8(const double x[8], double o[8]) {
+// One 8-point Arai pass, Dct.hpp:62-131 (same op order for both passes), up to
+// the final scaling: o[k] = w[k] * kS_k.
+__device__ __forceinline__ void arai8_unscaled(const double x[8], double w[8]) {
     double z0 = x[0] + x[7], z1 = x[1] + x[6], z2 = x[2] + x[5], z3 = x[3] + x[4];
     double z4 = -x[4] + x[3], z5 = -x[5] + x[2], z6 = -x[6] + x[1], z7 = -x[7] + x[0];
     double r0 = z0 + z3, r1 = z1 + z2, r2 = z1 - z2, r3 = z0 - z3;
@@ -36,28 +44,50 @@ __device__ __forceinline__ void arai8(const double x[8], double o[8]) {
     double u4 = -t4 - tmp, u6 = t6 - tmp;
     double v2 = t2 + r3, v3 = r3 - t2, v5 = t5 + r7, v7 = r7 - t5;
     double w4 = u4 + v7, w5 = v5 + u6, w6 = -u6 + v5, w7 = v7 - u4;
-    o[0] = t0 * kS0; o[4] = t1 * kS4; o[2] = v2 * kS2; o[6] = v3 * kS6;
-    o[5] = w4 * kS5; o[1] = w5 * kS1; o[7] = w6 * kS7; o[3] = w7 * kS3;
+    w[0] = t0; w[4] = t1; w[2] = v2; w[6] = v3;
+    w[5] = w4; w[1] = w5; w[7] = w6; w[3] = w7;
+}
+constexpr double kS[8] = {kS0, kS1, kS2, kS3, kS4, kS5, kS6, kS7};
+__device__ __forceinline__ void arai8(const double x[8], double o[8]) {
+    double w[8];
+    arai8_unscaled(x, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = w[k] * kS[k];
 }
 
-// quantize, Coding.hpp:92-94: (int)std::round(d / q) — correctly rounded fp64
-// division, then round half away from zero.  Fast path: r = d * (1/q) is within
-// 2^-52 |r| of the true quotient and |r| <= |d| < 2^15 (q >= 1, 8-bit samples), so
-// unless r lies within 2^-30 of a half-integer, rint(r) (ties-to-even, but r is no
-// tie) equals the reference's integer; integer boundaries are harmless (a quotient
-// on either side of k rounds to k either way).  e = r - rint(r) is exact, so a lane
-// near a half-integer is flagged by |e| > 0.5 - 2^-30 and the whole row is redone
-// by exact division (rare; one branch per row).
-__device__ __forceinline__ int quant_fast(double d, double invq, bool& near_half) {
-    const double r = d * invq;
+// quantize, Coding.hpp:92-94, of the row pass's output o = w * s_u (Dct.hpp:124-131):
+// (int)std::round(o / q) — two correctly rounded fp64 operations, then round half
+// away from zero.  Fast path: r = w * c with c = fl(s_u / q) is within 2^-51 |r| of
+// the reference's quotient fl(fl(w s_u) / q), and |r| < 2^11 (8-bit samples, q >= 1),
+// so the two differ by < 2^-40: unless r lies within 2^-30 of a half-integer, rint(r)
+// (ties-to-even, but r is no tie) is the reference's integer; integer boundaries are
+// harmless (a quotient on either side of k rounds to k either way).  e = r - rint(r)
+// is exact, so a lane near a half-integer is flagged by |e| > 0.5 - 2^-30 and the
+// whole row is redone the reference's way (rare; one branch per row).
+__device__ __forceinline__ int quant_fast(double w, double c, bool& near_half) {
+    const double r = w * c;
     const double k = __builtin_rint(r);
     near_half |= __builtin_fabs(r - k) > 0.5 - 0x1p-30;
     return (int)k;
 }
 
-__device__ __forceinline__ int quant_exact(double d, double q) { return (int)round(d / q); }
+__device__ __forceinline__ int quant_exact(double w, double s, double q) { return (int)round((w * s) / q); }
 
-constexpr int kK1Threads = 256;  // 4 waves, one 4-MCU tile each
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 as_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's range
+#ifndef K1_STORE_AUX
+#define K1_STORE_AUX 16  // sc1: write-through coefficient stores (no dirty L2 lines at the kernel's end)
+#endif
+#ifndef K1_LOAD_AUX
+#define K1_LOAD_AUX 0
+#endif
+
+// Workgroup shapes: 16 waves = one workgroup per CU (4 waves per SIMD), whose
+// waves balance their tiles among themselves — best when the kernel has the GPU to
+// itself; 4 waves = four workgroups per CU, which co-schedule beside other lanes'
+// kernels (a whole-CU workgroup waits for a whole CU to drain).
+constexpr int kK1WavesSolo = 16, kK1WavesShared = 4;
 constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
 constexpr int kTmpBlock = 72;    // doubles per transpose block (rows of 9 doubles)
 constexpr int kTmpRow = 9;
@@ -67,10 +97,12 @@ struct K1WaveLds {
     double tmp[8 * kTmpBlock];      // pass-1 output, transposed
 };
 constexpr int kQRow = 9;  // padded q-table rows: lanes reading rows j=0..7 hit distinct banks
+template <int kWaves>
 struct K1Lds {
-    K1WaveLds w[4];
+    K1WaveLds w[kWaves];
+    uint32_t next;  // next tile of the workgroup's run to hand out
     double q[2][8 * kQRow];     // luma, chroma
-    double invq[2][8 * kQRow];  // 1/q (correctly rounded)
+    double invq[2][8 * kQRow];  // s_u / q (correctly rounded), u = column
 };
 
 __device__ __forceinline__ double ycc_exact_y(uint32_t p) {
@@ -91,65 +123,156 @@ __device__ __forceinline__ double ycc_ref_c(uint32_t p, double scale, double kr,
     return (128.0 + ((kr * r + kg * g) + kb * b)) - 128;
 }
 
-template <bool kExact>
-__global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
-    __shared__ K1Lds lds;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+template <bool kExact, int kWaves>
+__global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
+    constexpr int kK1Threads = kWaves * 64;
+    __shared__ K1Lds<kWaves> lds;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;  // wv: 0..15
     K1WaveLds& W = lds.w[wv];
-    for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
-    if (blockIdx.x == 0)  // carried: another frame's tables + headers, host -> device
-        for (uint32_t i = tid; i < a.imp_n16; i += kK1Threads) a.imp_dst[i] = a.imp_src[i];
-    if (tid < 128) {
-        const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
-        const double q = (double)a.q[tid];  // Image.cpp:611-636 divides by the entry as double
-        lds.q[c][o] = q;
-        lds.invq[c][o] = 1.0 / q;
-    }
-    __syncthreads();
-    JPGE_STAMP(0);
-
+    JPGE_STAMP(1);
     const uint32_t mw = a.g.mw;
     const uint32_t tiles_per_row = (mw + 3) / 4;
     const uint32_t ntiles = tiles_per_row * a.g.mh;
-    const uint32_t nwaves = gridDim.x * 4;
     const double scale = 255.0 / (double)a.maxval;  // Image.cpp:465
     const bool aligned = (((uintptr_t)a.rgb | a.stride) & 15) == 0;
     const int r16 = lane >> 2, c16 = lane & 3;  // staging: lane -> (pixel row, 16-px chunk)
     const int b8 = lane >> 3, j = lane & 7;     // DCT: lane -> (block of the round, column)
 
-    // 48-byte RGB run of this lane for tile t, if the tile is on the aligned fast path
-    auto fast_load = [&](uint32_t t, uint4& v0, uint4& v1, uint4& v2) -> bool {
+    // Pixels and coefficients move through buffer descriptors: an out-of-range
+    // offset (kOob) makes a load return zeros and drops a store, so every tile
+    // issues the same 3 loads and 3 stores with no branch around them, and the
+    // wait for the prefetched pixels leaves the previous tile's stores in flight.
+    const __amdgpu_buffer_rsrc_t rgb_rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(a.rgb), 0, (int)(uint32_t)((uint64_t)a.stride * (a.g.height - 1) + 3ull * a.g.width),
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t coef_rs =
+        __builtin_amdgcn_make_buffer_rsrc(a.coef, 0, (int)(uint32_t)((uint64_t)a.g.nblocks() * 128), 0x00020000);
+
+    // Dynamic tiles.  One workgroup per CU owns a contiguous run of n_p tiles; each
+    // of its 16 waves takes its first tile by rank, then grabs more from an LDS
+    // counter until the run is exhausted.  The SIMD issues the oldest ready wave
+    // first, so waves progress unequally: grabbing lets the faster ones take more
+    // tiles, and all waves of a CU finish within about a tile of each other.
+    const uint32_t tb_p = (uint32_t)((uint64_t)ntiles * blockIdx.x / gridDim.x);
+    const uint32_t n_p = (uint32_t)((uint64_t)ntiles * (blockIdx.x + 1) / gridDim.x) - tb_p;
+    auto grab = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(&lds.next, 1u);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+
+    // 48-byte RGB run of this lane for partition tile k, if the tile is on the aligned
+    // fast path (else zeros, and the staging takes the clamped edge path)
+    auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
+        const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * 4;
         const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
-        if (!(aligned && y < a.g.height && xs + 16 <= a.g.width)) return false;
-        const uint4* src = reinterpret_cast<const uint4*>(a.rgb + (uint64_t)y * a.stride + (uint64_t)xs * 3);
-        v0 = src[0]; v1 = src[1]; v2 = src[2];
-        return true;
+        const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
+        const uint32_t off = ok ? (uint32_t)((uint64_t)y * a.stride + (uint64_t)xs * 3) : kOob;
+        v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
+        v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
+        v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, K1_LOAD_AUX));
+        return ok;
     };
-    uint32_t t = blockIdx.x * 4 + wv;
-    uint4 c0 = {}, c1 = {}, c2 = {};
-    bool cfast = t < ntiles && fast_load(t, c0, c1, c2);
+    // The last round's 16-byte coefficient row (kOob: none) is stored during the
+    // next tile, after its staging: the staging's wait for the prefetched pixels
+    // then finds only long-issued stores ahead of them in the in-order counter.
+    u32x4 pend;
+    uint32_t poff = kOob;
+    auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, K1_STORE_AUX); };
+    uint32_t k = wv;  // this wave's current tile of the run
+    uint4 c0, c1, c2;
+    bool cfast = fast_load(k, c0, c1, c2);  // issued before the prologue's own memory traffic
 
-    for (; t < ntiles; t += nwaves) {
+    for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
+    if (blockIdx.x == 0)  // carried: another frame's tables + headers, host -> device
+        for (uint32_t i = tid; i < a.imp_n16; i += kK1Threads) a.imp_dst[i] = a.imp_src[i];
+    if (tid == 0) lds.next = kWaves;
+    if (tid < 128) {
+        const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
+        const double q = (double)a.q[tid];  // Image.cpp:611-636 divides by the entry as double
+        lds.q[c][o] = q;
+        lds.invq[c][o] = kS[e & 7] / q;
+    }
+    __syncthreads();
+    JPGE_STAMP(0);
+    uint32_t kn = k < n_p ? grab() : n_p;  // the next tile (its pixels are prefetched a tile ahead)
+
+    // Round inputs, read from LDS in one batch per round (issued during the previous
+    // round's row pass): 8 pixel words of a Y column, or the 2x2 pixel pairs of 8
+    // chroma samples, and the lane's 8 reciprocal quantisers.
+    const int ycolbase = (b8 >> 2) * 16 + (b8 & 1) * 8 + j;  // Y round: column of the lane's block
+    const int yrow0 = ((b8 >> 1) & 1) * 8;
+    const int ccomp = b8 >> 2, cm = b8 & 3;
+    const int ccol = cm * 16 + 2 * j;
+    double* tb = &W.tmp[b8 * kTmpBlock];
+    auto load_y = [&](int round, uint32_t p[8]) {
+        const int col = round * 32 + ycolbase;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[i] = W.rgbx[(yrow0 + i) * kRgbPitch + col];
+    };
+    auto load_c = [&](uint2 c[16]) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = *reinterpret_cast<const uint2*>(&W.rgbx[i * kRgbPitch + ccol]);
+    };
+    auto load_iq = [&](int qb, double iq[8]) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) iq[u] = lds.invq[qb][j * kQRow + u];
+    };
+    auto y_inputs = [&](const uint32_t p[8], double x[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = kExact ? ycc_exact_y(p[i]) : ycc_ref_y(p[i], scale);
+    };
+    auto c_inputs = [&](const uint2 c[16], double x[8]) {
+        const double kr = ccomp ? kCrR : kCbR, kg = ccomp ? kCrG : kCbG, kb = ccomp ? kCrB : kCbB;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint2 t0 = c[2 * i], t1 = c[2 * i + 1];
+            if (kExact) {
+                // ((a+b)+(c+d))/4 of the exact per-pixel values equals the exact value
+                // of the channel sums
+                const uint32_t rb = (t0.x & 0xFF00FFu) + (t0.y & 0xFF00FFu) + (t1.x & 0xFF00FFu) + (t1.y & 0xFF00FFu);
+                const uint32_t all = t0.x + t0.y + t1.x + t1.y;  // fields overlap; G = (all - rb) >> 8
+                const double sr = (double)(rb & 0xFFFF), sb = (double)(rb >> 16), sg = (double)((all - rb) >> 8);
+                // (the 1/4 is folded into the constants: every product stays exact)
+                x[i] = __builtin_fma(kb * 0.25, sb, __builtin_fma(kg * 0.25, sg, (kr * 0.25) * sr));
+            } else {
+                // subsample(S420_m), Image.cpp:207-224: ((0+a+b) + (0+c+d)) / 4
+                double top = 0.0, bot = 0.0;
+                top += ycc_ref_c(t0.x, scale, kr, kg, kb);
+                top += ycc_ref_c(t0.y, scale, kr, kg, kb);
+                bot += ycc_ref_c(t1.x, scale, kr, kg, kb);
+                bot += ycc_ref_c(t1.y, scale, kr, kg, kb);
+                x[i] = (top + bot) / 4;
+            }
+        }
+    };
+
+    uint32_t ndone = 0;
+    for (; k < n_p; ++ndone) {
+        const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row;
         const uint32_t mcol0 = (t % tiles_per_row) * 4;
         const int nvalid = (int)min(4u, mw - mcol0);
         const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
-        // prefetch the next tile of this wave while this one is transformed
-        uint4 n0 = {}, n1 = {}, n2 = {};
-        const bool nfast = t + nwaves < ntiles && fast_load(t + nwaves, n0, n1, n2);
 
+        JPGE_STAMP(2 + min(ndone, 4u));
         // ---- stage 16 px per lane as packed u32 ----
+        // (the prefetched registers are consumed on every path, so no later wait on
+        // them can also drain the previous tile's coefficient stores)
         uint32_t px[16];
-        if (cfast) {
+        {
             const uint4 v0 = c0, v1 = c1, v2 = c2;
             const uint32_t wd[13] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, 0u};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int b0 = 3 * i, d = b0 >> 2, sh = 8 * (b0 & 3);
-                px[i] = (sh ? __builtin_amdgcn_alignbit(wd[d + 1], wd[d], sh) : wd[d]) & 0xFFFFFFu;
+                // bytes b0..b0+2 of the run, zero-extended (perm selector 0x0c = 0x00)
+                const uint32_t o8 = (uint32_t)(sh / 8);
+                px[i] = __builtin_amdgcn_perm(wd[d + 1], wd[d], 0x0C000000u | ((o8 + 2) << 16) | ((o8 + 1) << 8) | o8);
             }
-        } else {  // right/bottom edge replication (Image.cpp:498-531) as clamped addressing
+        }
+        if (!cfast) {  // right/bottom edge replication (Image.cpp:498-531) as clamped addressing
             const uint32_t sy = min(y, a.g.height - 1);
             for (int i = 0; i < 16; ++i) {
                 const uint32_t sx = min(xs + i, a.g.width - 1);
@@ -160,105 +283,113 @@ __global__ __launch_bounds__(kK1Threads) void fdct_kernel(FdctArgs a) {
         uint32_t* dst = &W.rgbx[r16 * kRgbPitch + c16 * 16];
 #pragma unroll
         for (int i = 0; i < 16; i += 2) *reinterpret_cast<uint2*>(dst + i) = make_uint2(px[i], px[i + 1]);
-        wave_lds_sync();
+        wave_order();
+        // prefetch the next tile of this wave (into the registers just staged) while
+        // this one is transformed
+        store_pending();
+        cfast = fast_load(kn, c0, c1, c2);
+        const uint32_t kn2 = kn < n_p ? grab() : n_p;
 
-        // ---- rounds: Y blocks 0-7, Y blocks 8-15, then Cb x4 + Cr x4 ----
-#pragma unroll 1
-        for (int round = 0; round < 3; ++round) {
-            double x[8];
-            int m, slot, qb;
-            if (round < 2) {
-                const int yb = round * 8 + b8, sub = yb & 3;
-                m = yb >> 2;
-                const int col = m * 16 + (sub & 1) * 8 + j, row0 = (sub >> 1) * 8;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint32_t p = W.rgbx[(row0 + i) * kRgbPitch + col];
-                    x[i] = kExact ? ycc_exact_y(p) : ycc_ref_y(p, scale);
-                }
-                slot = sub;
-                qb = 0;
-            } else {
-                const int comp = b8 >> 2;
-                m = b8 & 3;
-                const double kr = comp ? kCrR : kCbR, kg = comp ? kCrG : kCbG, kb = comp ? kCrB : kCbB;
-                const int col = m * 16 + 2 * j;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint2 t0 = *reinterpret_cast<const uint2*>(&W.rgbx[(2 * i) * kRgbPitch + col]);
-                    const uint2 t1 = *reinterpret_cast<const uint2*>(&W.rgbx[(2 * i + 1) * kRgbPitch + col]);
-                    if (kExact) {
-                        // ((a+b)+(c+d))/4 of the exact per-pixel values equals the exact
-                        // value of the channel sums
-                        const uint32_t s = (t0.x & 0xFF00FFu) + (t0.y & 0xFF00FFu) + (t1.x & 0xFF00FFu) +
-                                           (t1.y & 0xFF00FFu);
-                        const double sr = (double)(s & 0xFFFF), sb = (double)(s >> 16);
-                        const double sg = (double)(((t0.x >> 8) & 0xFF) + ((t0.y >> 8) & 0xFF) +
-                                                   ((t1.x >> 8) & 0xFF) + ((t1.y >> 8) & 0xFF));
-                        x[i] = __builtin_fma(kb, sb, __builtin_fma(kg, sg, kr * sr)) * 0.25;
-                    } else {
-                        // subsample(S420_m), Image.cpp:207-224: ((0+a+b) + (0+c+d)) / 4
-                        double top = 0.0, bot = 0.0;
-                        top += ycc_ref_c(t0.x, scale, kr, kg, kb);
-                        top += ycc_ref_c(t0.y, scale, kr, kg, kb);
-                        bot += ycc_ref_c(t1.x, scale, kr, kg, kb);
-                        bot += ycc_ref_c(t1.y, scale, kr, kg, kb);
-                        x[i] = (top + bot) / 4;
-                    }
-                }
-                slot = 4 + comp;
-                qb = 1;
-            }
-            // column pass, written transposed (Dct.hpp:124-131); row pass
+        // ---- rounds: Cb x4 + Cr x4, Y blocks 0-7 (MCUs 0, 1), Y blocks 8-15 (MCUs 2, 3) ----
+        // A round: inputs -> column pass -> transposed LDS write (Dct.hpp:124-131) ->
+        // row pass -> quantise -> one 16-byte row store.  A wave's LDS operations run
+        // in issue order, so only the compiler needs fencing between them.
+        // The chroma round's inputs are read now; each later round's during the
+        // previous round's row pass.
+        uint32_t p[8];
+        uint2 cc[16];
+        double iq[8];
+        load_c(cc);
+        load_iq(1, iq);
+        wave_order();
+        auto finish = [&](double x[8], int m, int slot, int qb, u32x4& pk, uint32_t& off, auto&& prefetch_next) {
             double o[8];
             arai8(x, o);
-            double* tb = &W.tmp[b8 * kTmpBlock];
 #pragma unroll
             for (int k = 0; k < 8; ++k) tb[j * kTmpRow + k] = o[k];
-            wave_lds_sync();
+            wave_order();
 #pragma unroll
             for (int i = 0; i < 8; ++i) x[i] = tb[i * kTmpRow + j];
-            arai8(x, o);  // o[u] = y(j, u)
+            double iqc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) iqc[u] = iq[u];
+            wave_order();
+            prefetch_next();  // next round's inputs: after this round's LDS reads
+            arai8_unscaled(x, o);  // y(j, u) = o[u] * s_u
             int qv[8];
             bool near_half = false;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) qv[u] = quant_fast(o[u], lds.invq[qb][j * kQRow + u], near_half);
+            for (int u = 0; u < 8; ++u) qv[u] = quant_fast(o[u], iqc[u], near_half);
             if (__builtin_amdgcn_ballot_w64(near_half)) {  // wave-uniform: a real branch, not predication
 #pragma unroll
-                for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], lds.q[qb][j * kQRow + u]);
+                for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], kS[u], lds.q[qb][j * kQRow + u]);
             }
-            if (m < nvalid) {
-                const uint64_t blk = ((uint64_t)mrow * mw + mcol0 + m) * 6 + slot;
-                uint4 pk;
-                pk.x = (uint32_t)(qv[0] & 0xFFFF) | ((uint32_t)qv[1] << 16);
-                pk.y = (uint32_t)(qv[2] & 0xFFFF) | ((uint32_t)qv[3] << 16);
-                pk.z = (uint32_t)(qv[4] & 0xFFFF) | ((uint32_t)qv[5] << 16);
-                pk.w = (uint32_t)(qv[6] & 0xFFFF) | ((uint32_t)qv[7] << 16);
-                *reinterpret_cast<uint4*>(a.coef + blk * 64 + j * 8) = pk;
-            }
-            wave_lds_sync();
+            const uint32_t blk = (mrow * mw + mcol0 + m) * 6 + slot;
+            off = m < nvalid ? blk * 128 + j * 16 : kOob;
+            pk.x = __builtin_amdgcn_perm((uint32_t)qv[1], (uint32_t)qv[0], 0x05040100u);
+            pk.y = __builtin_amdgcn_perm((uint32_t)qv[3], (uint32_t)qv[2], 0x05040100u);
+            pk.z = __builtin_amdgcn_perm((uint32_t)qv[5], (uint32_t)qv[4], 0x05040100u);
+            pk.w = __builtin_amdgcn_perm((uint32_t)qv[7], (uint32_t)qv[6], 0x05040100u);
+        };
+        {
+            double x[8];
+            c_inputs(cc, x);
+            u32x4 pk;
+            uint32_t off;
+            finish(x, cm, 4 + ccomp, 1, pk, off, [&] {
+                load_y(0, p);
+                load_iq(0, iq);
+            });
+            __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
         }
-        c0 = n0; c1 = n1; c2 = n2;
-        cfast = nfast;
+        {
+            double x[8];
+            y_inputs(p, x);
+            u32x4 pk;
+            uint32_t off;
+            finish(x, b8 >> 2, b8 & 3, 0, pk, off, [&] { load_y(1, p); });
+            __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
+        }
+        {
+            double x[8];
+            y_inputs(p, x);
+            finish(x, 2 + (b8 >> 2), b8 & 3, 0, pend, poff, [] {});
+        }
+        wave_order();  // the next tile's staging overwrites the transpose buffer
+        k = kn;
+        kn = kn2;
     }
+    store_pending();
     __syncthreads();
     JPGE_STAMP(7);
 }
 
 }  // namespace
 
-uint32_t fdct_grid(const Geometry& g) {
+uint32_t fdct_grid(const Geometry& g, bool solo) {
     const uint32_t tiles = ((g.mw + 3) / 4) * g.mh;
-    const uint32_t wgs = (tiles + 3) / 4;
-    return wgs < 1024 ? wgs : 1024;  // 4 workgroups per CU, persistent
+    // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
+    const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
+    const uint32_t cap = solo ? 256u : 1024u;
+    return wgs < cap ? wgs : cap;
 }
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
-    const uint32_t grid = fdct_grid(a.g);
-    if (a.maxval == 255)
-        hipLaunchKernelGGL(fdct_kernel<true>, dim3(grid), dim3(kK1Threads), 0, s, a);
-    else
-        hipLaunchKernelGGL(fdct_kernel<false>, dim3(grid), dim3(kK1Threads), 0, s, a);
+    // 32-bit buffer offsets: the frame's pixels and coefficients must stay below kOob
+    // (a 16384^2 frame needs 805 MB of each)
+    if ((uint64_t)a.stride * a.g.height >= kOob || (uint64_t)a.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
+    const uint32_t grid = fdct_grid(a.g, a.solo);
+    if (a.solo) {
+        if (a.maxval == 255)
+            hipLaunchKernelGGL((fdct_kernel<true, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+        else
+            hipLaunchKernelGGL((fdct_kernel<false, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+    } else {
+        if (a.maxval == 255)
+            hipLaunchKernelGGL((fdct_kernel<true, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        else
+            hipLaunchKernelGGL((fdct_kernel<false, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ struct FdctArgs {
     uint64_t stride;
     Geometry g;
     int maxval;      // 255 -> exact integer colour path
+    bool solo;       // the kernel has the GPU to itself: whole-CU workgroups (else 4-wave ones)
     uint8_t q[128];  // luma then chroma quantisers, natural order (bytes: a small kernarg block)
     int16_t* coef;
     uint32_t* zero;       // the frame's control block, zeroed by this kernel (it runs first)
@@ -143,7 +144,7 @@ inline uint32_t entropy_tiles(const Geometry& g) {
 // local offsets, worst case) plus slack, a whole number of 128-byte lines
 constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntropyTile * kStageBytesPerBlock + 128;
 
-uint32_t fdct_grid(const Geometry& g);
+uint32_t fdct_grid(const Geometry& g, bool solo);
 uint32_t stats_grid(const Geometry& g);
 uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override);
 
