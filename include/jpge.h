@@ -84,7 +84,16 @@ int jpge_reset_timing(jpge_ctx* ctx);
  * them (env JPGE_LANES at jpge_open, default 4). */
 int jpge_get_lanes(jpge_ctx* ctx, int* lanes);
 
-/* Worst-case .jpg size for a frame (header + 2x worst-case entropy + EOI). */
+/* Restart intervals for the context's following encodes (jpge_encode_rgb8, _batch,
+ * _file): every `mcus` MCUs the DC predictions restart and the entropy stream is
+ * 1-filled and followed by an RSTn marker, announced by a DRI segment before SOS
+ * (ITU T.81 B.2.4.4, F.1.2.3).  0 (the default) = none: the reference's stream,
+ * bit-identical to it.  Replaces nothing in the reference (writeJPEG never emits
+ * DRI/RSTn, Image.cpp:931-972); its decoded pixels equal the mcus = 0 output's.
+ * 1..65535, else JPGE_E_ARG; the stripe phases (jpge_stripe_*) need mcus = 0. */
+int jpge_set_restart_interval(jpge_ctx* ctx, uint32_t mcus);
+
+/* Worst-case .jpg size for a frame (header + 2x worst-case entropy + RST markers + EOI). */
 size_t jpge_max_jpeg_bytes(uint32_t width, uint32_t height);
 
 /* Quantisation tables for quality 1..100: the reference's Annex-K tables

@@ -31,7 +31,7 @@ STATUS = {
 # every symbol include/jpge.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_open_ex", "jpge_close", "jpge_set_timing",
-    "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
+    "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_set_restart_interval", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_synth_rgb8", "jpge_arai_constants",
     "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
@@ -97,6 +97,7 @@ def lib() -> ctypes.CDLL:
         L.jpge_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
         L.jpge_reset_timing.argtypes = [vp]
         L.jpge_get_lanes.argtypes = [vp, ctypes.POINTER(i32)]
+        L.jpge_set_restart_interval.argtypes = [vp, u32]
         L.jpge_device_count.argtypes = [ctypes.POINTER(i32)]
         L.jpge_max_jpeg_bytes.restype = sz
         L.jpge_max_jpeg_bytes.argtypes = [u32, u32]
@@ -270,6 +271,10 @@ class Encoder:
 
     def reset_timing(self) -> None:
         _check(lib().jpge_reset_timing(self._ctx), "reset_timing")
+
+    def set_restart(self, mcus: int) -> None:
+        """Restart interval in MCUs for the following encodes (0 = none: the reference's stream)."""
+        _check(lib().jpge_set_restart_interval(self._ctx, int(mcus)), "set_restart_interval")
 
     def lanes(self) -> int:
         n = ctypes.c_int32()

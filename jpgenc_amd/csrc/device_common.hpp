@@ -141,10 +141,15 @@ struct TileRegs {
     }
 };
 
-// DC of the chain predecessor of block b0+blk (0 for a chain's first block), from
-// the staged tile or the 6 DCs staged before it.
+// DC of the chain predecessor of block b0+blk (0 for a chain's first block and at a
+// restart interval's start), from the staged tile or the 6 DCs staged before it.
 __device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, const int* prevdc,
-                                       const DcSeed& seed) {
+                                       const DcSeed& seed, const Restart& rs) {
+    if (rs.mcus) {  // a restart interval's first MCU: Y00, Cb and Cr predict 0 again
+        const uint64_t g = b0 + blk;
+        const int k = (int)(g % 6);
+        if ((k == 0 || k >= 4) && (g / 6 + rs.mcu0) % rs.mcus == 0) return 0;
+    }
     const int64_t pg = dc_pred_index(b0 + blk);
     if (pg < 0) {  // first MCU: the chain starts at 0, or at the previous stripe's last DC
         const int k = (int)((b0 + blk) % 6);

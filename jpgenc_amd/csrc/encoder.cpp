@@ -99,7 +99,7 @@ constexpr size_t kHdrMax = 4096;           // headers SOI .. SOS (<= 20 + 2*69 +
 struct CtlLayout {
     size_t cnt, key, rec, total;  // [0, total): zeroed by K1 every frame
     size_t place, summary, alloc;  // not zeroed (written before they are read)
-    explicit CtlLayout(uint32_t ntiles) {  // (entropy workgroups <= entropy tiles)
+    explicit CtlLayout(uint32_t ntiles) {  // ntiles: entropy workgroups (records)
         size_t o = 0;
         cnt = o; o += align_up((size_t)kHistReplicas * 4 * 256 * 4, 256);
         key = o; o += align_up(4 * 256 * 8, 256);
@@ -293,11 +293,18 @@ struct Encoder::Lane {
     }
 };
 
+int Encoder::set_restart(uint32_t mcus) {
+    if (mcus > 65535) return kErrArg;  // DRI carries a 16-bit interval
+    restart_mcus_ = mcus;
+    return kOk;
+}
+
 size_t Encoder::max_jpeg_bytes(uint32_t w, uint32_t h) {
     // header <= 20 + 2*69 + 19 + 4*(4+17+256) + 14 ; entropy <= 1665 bits/block,
     // doubled for worst-case 0xFF stuffing; + EOI.
+    // Restart intervals add per MCU at most an RST marker, a fill byte and its stuffing.
     const Geometry g = geometry(w, h);
-    return 2048 + (size_t)g.nblocks() * 2 * 209 + 16;
+    return 2048 + (size_t)g.nblocks() * 2 * 209 + 16 + (size_t)g.nmcu() * 4;
 }
 
 int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
@@ -377,8 +384,8 @@ void Encoder::dump_stamps(const Slot& s) {
     if (!stamps_file_ || !d_dbg_) return;
     std::vector<uint64_t> h(dbg_words_);
     if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(s.g), entropy_grid(s.g, entropy_wgs_),
-                             entropy_grid(s.g, entropy_wgs_)};
+    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(s.g), layout(s.g).grid(),
+                             layout(s.g).grid()};
     FILE* f = std::fopen(stamps_file_, "wb");
     if (!f) return;
     std::fwrite(hdr, 8, 4, f);
@@ -395,8 +402,8 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         JPGE_HIP(hipMalloc((void**)&s.d_coef, nmcu * 768));
         s.cap_mcu = nmcu;
     }
-    const CtlLayout L(entropy_tiles(g));
-    const size_t ubuf = entropy_ubuf_bytes(g, entropy_wgs_);
+    const CtlLayout L(layout(g).grid());
+    const size_t ubuf = entropy_ubuf_bytes(layout(g));
     if (ubuf > s.cap_ubuf) {
         hipFree(s.d_ubuf); s.d_ubuf = nullptr; s.cap_ubuf = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_ubuf, ubuf));
@@ -422,7 +429,7 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
 
 // Kernel parameter blocks of a slot's frame (or stripe).
 FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
-    const CtlLayout L(entropy_tiles(s.g));
+    const CtlLayout L(layout(s.g).grid());
     FdctArgs a;
     a.rgb = s.in_dev;
     a.stride = s.in_stride;
@@ -444,13 +451,14 @@ FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
 }
 
 StatsArgs Encoder::stats_args(Slot& s) {
-    const CtlLayout L(entropy_tiles(s.g));
+    const CtlLayout L(layout(s.g).grid());
     StatsArgs st;
     st.coef = s.d_coef;
     st.g = s.g;
     st.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
     st.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
     st.seed = s.seed;
+    st.rst.mcus = restart_mcus_;
     st.key_y0 = s.key_y0;
     st.key_c0 = s.key_c0;
     st.key_ncb = s.key_ncb;
@@ -459,7 +467,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
 }
 
 EntropyArgs Encoder::entropy_args(Slot& s) {
-    const CtlLayout L(entropy_tiles(s.g));
+    const CtlLayout L(layout(s.g).grid());
     EntropyArgs e;
     e.coef = s.d_coef;
     e.g = s.g;
@@ -477,6 +485,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.wgs = entropy_wgs_;
     e.diag = diag_;
     e.seed = s.seed;
+    e.rst.mcus = restart_mcus_;
+    e.seg = layout(s.g);
     e.exp_hist = HistPtrs{};
     e.exp_cnt = nullptr;
     e.exp_key = nullptr;
@@ -574,7 +584,7 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
     if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
-    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp);
+    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_);
     if (hdr.size() > kHdrMax) return kErrInternal;
     std::memcpy(reinterpret_cast<uint8_t*>(s.h_tab) + kTabBytes, hdr.data(), hdr.size());
     s.hdr_len = hdr.size();
@@ -875,6 +885,7 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
 // lane 0's first slot and returns when its results are on the host.
 int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]) {
     JPGE_HIP(hipSetDevice(device_));
+    if (restart_mcus_) return kErrArg;  // (the stripe phases run the reference's single interval)
     if (!d.rgb || !last_dc || d.width == 0 || d.height == 0 || d.width > 65535 || d.height > 65535) return kErrArg;
     if (d.maxval < 1 || d.maxval > 255) return kErrRange;
     const uint32_t mh_img = (d.height + 15) / 16;
@@ -911,6 +922,7 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
 
 int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t first[1024]) {
     JPGE_HIP(hipSetDevice(device_));
+    if (restart_mcus_) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !seed || !counts || !first) return kErrArg;
     for (int c = 0; c < 3; ++c) s.seed.v[c] = seed[c];
@@ -931,6 +943,7 @@ int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t
 int Encoder::stripe_code(const uint32_t counts[1024], const uint64_t first[1024], StripeSummary* sum,
                          size_t* hdr_len) {
     JPGE_HIP(hipSetDevice(device_));
+    if (restart_mcus_) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !counts || !first || !sum) return kErrArg;
     s.out_dev = nullptr;
@@ -981,6 +994,7 @@ int Encoder::stripe_place(const StripeSummary* all, int n, int index, size_t hdr
 int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* out_dev, size_t cap, size_t* seg_off,
                          size_t* seg_len, size_t* total_len) {
     JPGE_HIP(hipSetDevice(device_));
+    if (restart_mcus_) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !out_dev || !s.hdr_len) return kErrArg;
     uint64_t p_ext = 0, q_ext = 0;

@@ -85,6 +85,10 @@ class Encoder {
     const KernelTimes& times() const { return times_; }
     int device() const { return device_; }
     static size_t max_jpeg_bytes(uint32_t w, uint32_t h);
+    // restart interval in MCUs for the following encodes (0 = none, the reference's
+    // stream); not for the stripe phases
+    int set_restart(uint32_t mcus);
+    uint32_t restart() const { return restart_mcus_; }
 
     int lanes() const { return (int)lanes_.size(); }
 
@@ -118,6 +122,8 @@ class Encoder {
     std::atomic<uint64_t> seq_counter_{0};
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
+    uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
+    SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs_); }
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain

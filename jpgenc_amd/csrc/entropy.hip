@@ -112,7 +112,7 @@ struct PartCoder {
 };
 
 __device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int nb, int blk, int part,
-                                                const DcSeed& seed) {
+                                                const DcSeed& seed, const Restart& rs) {
     PartCoder c;
     c.part = part;
     c.active = blk < nb;
@@ -122,7 +122,7 @@ __device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int
     c.mask = c.active ? L.bmask[blk] : 0ull;
     c.pv.load(L.u.zz, c.mask, blk, part, c.active);
     // DC difference to the chain predecessor, Image.cpp:638-678
-    c.dcdiff = (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc, seed) : 0;
+    c.dcdiff = (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc, seed, rs) : 0;
     return c;
 }
 
@@ -153,12 +153,6 @@ __device__ __forceinline__ uint32_t code_part(const PartCoder& c, SlotSink& bs) 
     return bs.finish();
 }
 
-__device__ __forceinline__ void tile_range(const Geometry& g, uint32_t w, uint32_t G, uint32_t& tf, int& ntl) {
-    const uint32_t ntiles = (g.nblocks() + kK3Blocks - 1) / kK3Blocks;
-    tf = (uint32_t)((uint64_t)w * ntiles / G);
-    ntl = (int)((uint64_t)(w + 1) * ntiles / G) - (int)tf;  // 1..kMaxTiles (entropy_grid)
-}
-
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_code_kernel(
     EntropyArgs a) {
     __shared__ K3Lds L;
@@ -171,31 +165,30 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
-    const uint32_t nblocks = a.g.nblocks();
-    uint32_t tf;
-    int ntl;
-    tile_range(a.g, wg, gridDim.x, tf, ntl);
+    const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
+    const int ntl = (int)wt.nt;
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
-    auto tile_nb = [&](uint32_t t) { return (int)min((uint64_t)kK3Blocks, nblocks - (uint64_t)t * kK3Blocks); };
+    auto tile_b0 = [&](int lt) { return wt.tile_b0(wt.t0 + lt); };
+    auto tile_nb = [&](int lt) { return (int)wt.tile_nb(wt.t0 + lt); };
 
     // ---- emit every tile at workgroup-local bit offsets into R ----
     TileRegs<kK3Threads, kK3Blocks> regs;
     regs.init(tid);
-    regs.load(a.coef, (uint64_t)tf * kK3Blocks, tile_nb(tf), tid);
+    regs.load(a.coef, tile_b0(0), tile_nb(0), tid);
     uint32_t wl = 0;  // workgroup-local bit position of the current tile
     uint64_t tq = JPGE_NOW();
     for (int lt = 0; lt < ntl; ++lt) {
-        const uint64_t b0 = (uint64_t)(tf + lt) * kK3Blocks;
-        const int nb = tile_nb(tf + lt);
+        const uint64_t b0 = tile_b0(lt);
+        const int nb = tile_nb(lt);
         __syncthreads();  // previous tile: stage stored, carry set (u is free); tables loaded
         regs.stage(nb, L.u.zz, L.bmask, L.prevdc, tid);
-        if (lt + 1 < ntl) regs.load(a.coef, b0 + kK3Blocks, tile_nb(tf + lt + 1), tid);
+        if (lt + 1 < ntl) regs.load(a.coef, tile_b0(lt + 1), tile_nb(lt + 1), tid);
         __syncthreads();
         JPGE_ACC(0, tq);
         uint32_t n;  // bits of this lane's part
         {
-            const PartCoder pc = make_coder(L, b0, nb, blk, part, a.seed);
+            const PartCoder pc = make_coder(L, b0, nb, blk, part, a.seed, a.rst);
             SlotSink ss;
             ss.init(L.slot + tid);
             n = code_part(pc, ss);
@@ -364,11 +357,74 @@ __device__ __forceinline__ WgPlace make_place(const RecView& R, uint32_t k, uint
     w.ftotal = owned;
     w.split = b ? split_byte(R, k, b, a) : 0u;
     w.fill = (k == R.G - 1 && (a.flags & kStripeLast) && eb) ? fill_byte(eb, edge) : 0u;
-    w.pad = 0;
+    w.seg = 0;
     return w;
 }
 
 constexpr int kScanThreads = 1024;
+
+// Restart mode (a.rst.mcus != 0): segment-aligned placement.  Each segment (restart
+// interval) starts on a byte boundary; its last workgroup owns the segment's
+// 1-filled final byte; inside a segment the records split bytes as above.  Thread t
+// takes whole segments [t*per, (t+1)*per).  P counts entropy bits (each segment
+// rounded up to a whole byte), Q the 0x00 stuffing bytes before; the pack kernel
+// adds 2 bytes per RST marker before the workgroup's segment.
+__device__ void place_restart(const EntropyArgs& a, const RecView& R, uint32_t* wsum, int tid) {
+    constexpr int kW = kScanThreads / 64;
+    const int lane = tid & 63, wv = tid >> 6;
+    const SegLayout& L = a.seg;
+    const uint32_t per = (L.nseg + kScanThreads - 1) / kScanThreads;
+    const uint32_t s0 = min(L.nseg, tid * per), s1 = min(L.nseg, s0 + per);
+    auto rec0 = [&](uint32_t s) { return s * L.wps; };
+    auto nrec = [&](uint32_t s) { return s + 1 < L.nseg ? L.wps : L.lwps; };
+    uint64_t lsum = 0;
+    for (uint32_t s = s0; s < s1; ++s) {
+        uint64_t t = 0;
+        for (uint32_t k = rec0(s); k < rec0(s) + nrec(s); ++k) t += R(k)[kRecBits];
+        lsum += (t + 7) & ~7ull;
+    }
+    uint64_t ptot;
+    const uint64_t pbase = block_scan<kW>(lsum, wsum, lane, wv, ptot);
+    // 0xFF bytes record k owns when its stream starts at bit p: inside bytes at its
+    // alignment, the byte split with its predecessor (b != 0: never a segment's first
+    // record), the segment's 1-filled final byte
+    auto owned = [&](uint32_t s, uint32_t k, uint64_t p, uint32_t& split, uint32_t& fill) -> uint32_t {
+        const uint32_t* r = R(k);
+        const uint32_t b = (uint32_t)(p & 7), eb = (uint32_t)((p + r[kRecBits]) & 7);
+        uint32_t f = r[b];
+        split = b ? split_bits((R(k - 1)[kRecEdge] >> 8) & 0xFF, r[kRecEdge], b) : 0u;
+        fill = (k == rec0(s) + nrec(s) - 1 && eb) ? fill_byte(eb, r[kRecEdge]) : 0u;
+        return f + (b && split == 0xFF) + (fill == 0xFF);
+    };
+    uint64_t fsum = 0;
+    {
+        uint64_t p = pbase;
+        for (uint32_t s = s0; s < s1; ++s) {
+            for (uint32_t k = rec0(s); k < rec0(s) + nrec(s); ++k) {
+                uint32_t sp, fl;
+                fsum += owned(s, k, p, sp, fl);
+                p += R(k)[kRecBits];
+            }
+            p = (p + 7) & ~7ull;
+        }
+    }
+    uint64_t ftot;
+    const uint64_t fbase = a.q_ext + block_scan<kW>(fsum, wsum, lane, wv, ftot);
+    uint64_t p = pbase, q = fbase;
+    for (uint32_t s = s0; s < s1; ++s) {
+        for (uint32_t k = rec0(s); k < rec0(s) + nrec(s); ++k) {
+            WgPlace w;
+            w.P = p;
+            w.Q = q;
+            w.ftotal = owned(s, k, p, w.split, w.fill);
+            w.seg = s;
+            a.place[k] = w;
+            q += w.ftotal;
+            p += R(k)[kRecBits];
+        }
+        p = (p + 7) & ~7ull;
+    }
+}
 
 // entropy_scan_kernel — one workgroup over all G records.  Place mode: every
 // workgroup's WgPlace (large grids, stripes).  Summary mode: the stripe's bits,
@@ -378,6 +434,10 @@ __global__ __launch_bounds__(kScanThreads) void entropy_scan_kernel(EntropyArgs 
     __shared__ uint32_t tot8[8];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const RecView R{a.rec, G};
+    if (!summary && a.rst.mcus) {
+        place_restart(a, R, wsum, tid);
+        return;
+    }
     if (!summary) {
         scan_records<kScanThreads / 64>(a, R, wsum, tid, [&](uint32_t k, uint64_t p, uint64_t q, uint32_t o) {
             a.place[k] = make_place(R, k, p, q, o, a);
@@ -428,7 +488,7 @@ struct PackLds {
     uint8_t ob[2 * kChunk + 8];  // stuffed output of one round
     uint32_t wsum[2 * kK3Waves];  // (room for 64-bit scans)
     uint64_t P, Q;
-    uint32_t Lb, ftotal, split, fill;
+    uint32_t Lb, ftotal, split, fill, seg;
 };
 
 __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a) {
@@ -437,6 +497,9 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
     const uint32_t wg = blockIdx.x, G = gridDim.x;
     const bool last = wg == G - 1;
     const bool eoi = last && (a.flags & kStripeLast);
+    // the workgroup 1-fills its final byte: the image's end, or (restart) its segment's
+    const WgTiles wt = wg_tiles(a.seg, wg);
+    const bool fills = a.rst.mcus ? wt.last : eoi;
     JPGE_STAMP(0);
     if (wg == 0 && (a.flags & kStripeFirst)) {  // the headers (SOI .. SOS) travel behind the tables
         const uint8_t* hdr = reinterpret_cast<const uint8_t*>(a.tables + 1024);
@@ -453,6 +516,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
             S.ftotal = w.ftotal;
             S.split = w.split;
             S.fill = w.fill;
+            S.seg = w.seg;
             S.Lb = R(wg)[kRecBits];
         }
     } else {
@@ -464,6 +528,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
             S.ftotal = w.ftotal;
             S.split = w.split;
             S.fill = w.fill;
+            S.seg = 0;
             S.Lb = R(k)[kRecBits];
         });
     }
@@ -475,10 +540,15 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
     const uint32_t b = (uint32_t)(P & 7), Lb = S.Lb, ftotal = S.ftotal;
     const uint32_t nc = (b + Lb) >> 3;  // complete output bytes
     const uint32_t eb = (b + Lb) & 7;   // bits in the byte after them
-    const uint32_t n_own = nc + ((eoi && eb) ? 1u : 0u);
-    const uint64_t D0 = a.hdr_len + (P >> 3) + S.Q;
+    const uint32_t n_own = nc + ((fills && eb) ? 1u : 0u);
+    const uint32_t markers = a.rst.mcus ? S.seg + a.seg_markers0 : 0u;  // RST markers before this segment
+    const uint64_t D0 = a.hdr_len + (P >> 3) + S.Q + 2ull * markers;
     const uint64_t ntot = (uint64_t)n_own + ftotal + (eoi ? 2u : 0u);
     const bool fits = D0 + ntot <= a.out_cap;
+    if (fits && wt.first && markers && tid == 0) {  // RSTn ahead of the segment (not stuffed)
+        a.out[D0 - 2] = 0xFF;
+        a.out[D0 - 1] = (uint8_t)(0xD0 + ((markers - 1) & 7));
+    }
     const uint32_t split = S.split, fill = S.fill;
     const uint32_t* R32 = reinterpret_cast<const uint32_t*>(a.ubuf + (uint64_t)wg * kEntropyRegionBytes);
     const uint32_t nwr = (Lb + 31) >> 5;
@@ -500,7 +570,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
                 prev = cur;
             }
             if (j0 == 0 && b) y[0] = (y[0] & 0x00FFFFFFu) | (split << 24);
-            if (eoi && eb && n_own - 1 < j0 + kWin) {
+            if (fills && eb && n_own - 1 < j0 + kWin) {
                 const uint32_t q = n_own - 1 - j0, sh = 24 - 8 * (q & 3);
 #pragma unroll
                 for (int m = 0; m < kWinWords; ++m)
@@ -534,7 +604,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
         for (uint32_t w = tid; w < nw; w += kK3Threads) {
             const uint32_t s = 4 * w, e = s + 4;
             if (s >= align && e <= align + clen) {
-                *reinterpret_cast<uint32_t*>(gout + s) = *reinterpret_cast<const uint32_t*>(S.ob + s);
+                __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(S.ob + s), reinterpret_cast<uint32_t*>(gout + s));
             } else {
                 for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = S.ob[q];
             }
@@ -564,25 +634,53 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
 
 }  // namespace
 
-// Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size), at least two
-// each when the frame has two tiles (so a workgroup's stream holds >= 8 bits and
-// its split first byte and last byte differ); 512 = two per CU (LDS, registers).
-uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) {
-    const uint32_t nt = entropy_tiles(g);
-    if (nt <= 1) return 1;
-    const uint32_t lo = (nt + kMaxTiles - 1) / kMaxTiles, hi = nt / 2;
+// Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size); about 512 in
+// all (two per CU: LDS, registers) unless overridden.  One segment (restart off):
+// 128-block tiles, at least two per workgroup when the frame has two (so a
+// workgroup's stream holds >= 8 bits: its first and last 8 bits, which the
+// placement reads, are defined).  Restart intervals of R MCUs: segments of 6R
+// blocks (>= 6 blocks, >= 12 bits), each cut into balanced tiles of <= 128 blocks,
+// a whole number of workgroups per segment.
+SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override) {
+    SegLayout L;
+    const uint32_t nb = g.nblocks();
     const uint32_t want = wgs_override ? wgs_override : 512u;
-    return want < lo ? lo : (want > hi ? hi : want);
+    const uint64_t S = 6ull * restart_mcus;
+    if (!restart_mcus || S >= nb) {
+        const uint32_t nt = (nb + kK3Blocks - 1) / kK3Blocks;
+        uint32_t G = 1;
+        if (nt > 1) {
+            const uint32_t lo = (nt + kMaxTiles - 1) / kMaxTiles, hi = nt / 2;
+            G = want < lo ? lo : (want > hi ? hi : want);
+        }
+        L.nseg = 1;
+        L.sblk = L.lblk = nb;
+        L.tps = L.ltps = nt;
+        L.wps = L.lwps = G;
+        return L;
+    }
+    L.nseg = (uint32_t)((nb + S - 1) / S);
+    L.sblk = (uint32_t)S;
+    L.lblk = nb - (L.nseg - 1) * L.sblk;
+    const uint32_t per_seg = (want + L.nseg - 1) / L.nseg;
+    auto part = [&](uint32_t blocks, uint32_t& tps, uint32_t& wps) {
+        tps = (blocks + kK3Blocks - 1) / kK3Blocks;  // balanced tiles: >= 64 blocks each when tps > 1
+        const uint32_t lo = (tps + kMaxTiles - 1) / kMaxTiles;
+        wps = per_seg < lo ? lo : (per_seg > tps ? tps : per_seg);
+    };
+    part(L.sblk, L.tps, L.wps);
+    part(L.lblk, L.ltps, L.lwps);
+    return L;
 }
 
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
-    const uint32_t G = entropy_grid(a.g, a.wgs);
+    const uint32_t G = a.seg.grid();
     hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
-    if (G > kInlineScanMaxWgs || (a.flags & kExtPlace)) {
+    if (G > kInlineScanMaxWgs || (a.flags & kExtPlace) || a.rst.mcus) {
         if (!a.place) return hipErrorInvalidValue;
         b.flags |= kExtPlace;
         hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
@@ -593,7 +691,7 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
-    const uint32_t G = entropy_grid(a.g, a.wgs);
+    const uint32_t G = a.seg.grid();
     if (!a.summary) return hipErrorInvalidValue;
     hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
     hipError_t e = hipGetLastError();
@@ -603,7 +701,7 @@ hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s) {
-    const uint32_t G = entropy_grid(a.g, a.wgs);
+    const uint32_t G = a.seg.grid();
     if (!a.place) return hipErrorInvalidValue;
     EntropyArgs b = a;
     b.flags |= kExtPlace;

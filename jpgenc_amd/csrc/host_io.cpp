@@ -138,7 +138,7 @@ void quality_tables(int q, uint8_t qy[64], uint8_t qc[64]) {
 }
 
 std::vector<uint8_t> jfif_headers(uint32_t rw, uint32_t rh, const uint8_t qy[64], const uint8_t qc[64],
-                                  const HuffTable* const tables[4]) {
+                                  const HuffTable* const tables[4], uint32_t restart_mcus) {
     std::vector<uint8_t> o;
     o.reserve(700);
     // sSOI + sAPP0 (JpegSegments.hpp:55-109): JFIF 1.1, no units, density 1x1.
@@ -164,6 +164,9 @@ std::vector<uint8_t> jfif_headers(uint32_t rw, uint32_t rh, const uint8_t qy[64]
         o.push_back(0xFF); o.push_back(0xC4); put16(o, (uint32_t)(2 + 17 + t.nsym)); o.push_back(kInfo[k]);
         for (int l = 1; l <= 16; ++l) o.push_back(t.bits[l]);
         o.insert(o.end(), t.huffval, t.huffval + t.nsym);
+    }
+    if (restart_mcus) {  // DRI (ITU T.81 B.2.4.4): restart interval in MCUs
+        o.push_back(0xFF); o.push_back(0xDD); put16(o, 4); put16(o, restart_mcus & 0xFFFF);
     }
     // sSOS (JpegSegments.hpp:322-358): Y tables 0/0, Cb and Cr 1/1, Ss 0 Se 63 AhAl 0.
     static const uint8_t kSos[14] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x00, 0x02, 0x11, 0x03, 0x11, 0x00, 0x3F, 0x00};

@@ -69,11 +69,62 @@ struct DcSeed {
     int v[3] = {0, 0, 0};  // DC chain predecessors of the first Y / Cb / Cr block (Image.cpp:638-678)
 };
 
+// Restart intervals (DRI / RSTn; opt-in, not in the reference):
+// every `mcus` MCUs the DC predictions restart at 0, and the entropy stream is
+// 1-filled to a byte boundary and followed by an RSTn marker (n = interval - 1 mod 8).
+// mcus = 0: off (the reference's single interval).  mcu0: the frame's first MCU in
+// the image's numbering (a stripe starts at an interval boundary).
+struct Restart {
+    uint32_t mcus = 0;
+    uint32_t mcu0 = 0;
+};
+
+// The entropy kernels' partition of a frame: segments (restart intervals; one
+// segment when restart is off), each cut into tiles of <= kEntropyTile blocks
+// (balanced: tile i of a segment of nb blocks in tps tiles is blocks
+// [i*nb/tps, (i+1)*nb/tps)), each run of tiles owned by one workgroup.  A
+// workgroup's stream never crosses a segment boundary, so every segment starts
+// byte-aligned after its predecessor's fill.
+struct SegLayout {
+    uint32_t nseg = 1;                    // segments
+    uint32_t sblk = 0, tps = 0, wps = 0;  // a full segment: blocks, tiles, workgroups
+    uint32_t lblk = 0, ltps = 0, lwps = 0;  // the last segment (the frame's tail)
+    JPGE_HD uint32_t grid() const { return (nseg - 1) * wps + lwps; }
+};
+
+// Workgroup w's tiles: tiles [t0, t0 + nt) of segment seg (blocks [b0, b0 + nb) of
+// the frame, in tps tiles).
+struct WgTiles {
+    uint64_t b0;
+    uint32_t nb, tps, t0, nt, seg;
+    bool first, last;  // the segment's first / last workgroup
+    JPGE_HD uint64_t tile_b0(uint32_t i) const { return b0 + (uint64_t)i * nb / tps; }
+    JPGE_HD uint32_t tile_nb(uint32_t i) const {
+        return (uint32_t)((uint64_t)(i + 1) * nb / tps - (uint64_t)i * nb / tps);
+    }
+};
+JPGE_HD inline WgTiles wg_tiles(const SegLayout& L, uint32_t w) {
+    WgTiles r;
+    uint32_t j, wps;
+    if (w < (L.nseg - 1) * L.wps) {
+        r.seg = w / L.wps; j = w % L.wps; r.tps = L.tps; wps = L.wps; r.nb = L.sblk;
+    } else {
+        r.seg = L.nseg - 1; j = w - (L.nseg - 1) * L.wps; r.tps = L.ltps; wps = L.lwps; r.nb = L.lblk;
+    }
+    r.b0 = (uint64_t)r.seg * L.sblk;
+    r.t0 = (uint32_t)((uint64_t)j * r.tps / wps);
+    r.nt = (uint32_t)((uint64_t)(j + 1) * r.tps / wps) - r.t0;
+    r.first = j == 0;
+    r.last = j == wps - 1;
+    return r;
+}
+
 struct StatsArgs {
     const int16_t* coef;
     Geometry g;
     HistPtrs hist;
     DcSeed seed;
+    Restart rst;
     // first-occurrence key bases in the whole image's texts (Image.cpp:888-906):
     // Y raster index of the stripe's first Y block, Cb raster index of its first
     // Cb block, and the image's Cb block count (every Cr key follows all Cb keys)
@@ -87,8 +138,8 @@ struct alignas(16) WgPlace {
     uint64_t Q;       // 0x00 stuffing bytes before its first owned byte
     uint32_t ftotal;  // 0xFF bytes it owns (its stuffing count)
     uint32_t split;   // value of its first byte when shared with the predecessor (P & 7 != 0)
-    uint32_t fill;    // its 1-filled final byte (the image's last workgroup)
-    uint32_t pad;
+    uint32_t fill;    // its 1-filled final byte (the last workgroup of a restart interval / the image)
+    uint32_t seg;     // restart mode: its segment; the RST markers before its bytes = seg + seg_markers0
 };
 
 // A stripe's entropy summary (entropy_scan_kernel, summary mode): enough for the
@@ -132,8 +183,11 @@ struct EntropyArgs {
     uint64_t p_ext = 0, q_ext = 0;
     uint32_t head_split = 0;
     uint32_t flags = kStripeFirst | kStripeLast;
-    WgPlace* place = nullptr;          // [entropy_grid] (kExtPlace)
+    WgPlace* place = nullptr;          // [seg.grid()] (kExtPlace)
     StripeSummary* summary = nullptr;  // summary mode output
+    Restart rst;                       // restart intervals (rst.mcus = 0: none)
+    SegLayout seg;                     // workgroup partition (host: seg_layout)
+    uint32_t seg_markers0 = 0;         // RST markers before the frame's first segment (stripes)
     uint64_t* dbg;
 };
 
@@ -146,11 +200,12 @@ constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntr
 
 uint32_t fdct_grid(const Geometry& g, bool solo);
 uint32_t stats_grid(const Geometry& g);
-uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override);
+// entropy partition of a frame: restart_mcus = 0 -> one segment over 128-block tiles
+// (2..kEntropyMaxTilesPerWg per workgroup, about 512 workgroups or wgs_override)
+SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override);
+inline uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) { return seg_layout(g, 0, wgs_override).grid(); }
 
-inline uint64_t entropy_ubuf_bytes(const Geometry& g, uint32_t wgs_override) {
-    return (uint64_t)entropy_grid(g, wgs_override) * kEntropyRegionBytes;
-}
+inline uint64_t entropy_ubuf_bytes(const SegLayout& L) { return (uint64_t)L.grid() * kEntropyRegionBytes; }
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);

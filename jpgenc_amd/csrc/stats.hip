@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         PartView pv;
         pv.load(lds.zz, mask, blk, part, active);
         if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
-            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed));
+            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst));
             atomicAdd(&lds.dcnt[tsel][dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);

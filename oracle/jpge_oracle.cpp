@@ -382,6 +382,27 @@ void dc_diff(Frame& f) {
     }
 }
 
+// Restart-interval variant (not in the reference, which never emits DRI/RSTn): the
+// same chains with every predictor reset to 0 at the first MCU of each interval of R
+// MCUs (ITU T.81 F.1.2.3; MCU raster order is each chain's order at 4:2:0).
+void dc_diff_restart(Frame& f, int R) {
+    int bY = 0, bCb = 0, bCr = 0, m = 0;
+    const int cbw = f.sw / 8;
+    for (int h = 0; h < f.H; h += 16)
+        for (int w = 0; w < f.W; w += 16, ++m) {
+            if (m % R == 0) bY = bCb = bCr = 0;
+            const int off[4][2] = {{0, 0}, {0, 8}, {8, 0}, {8, 8}};
+            for (auto& o : off) {
+                int& v = f.qY[(size_t)(h + o[0]) * f.W + w + o[1]];
+                int t = v; v = t - bY; bY = t;
+            }
+            const size_t c = (size_t)(h / 2) * f.sw + w / 2;
+            (void)cbw;
+            int& vb = f.qCb[c]; int tb = vb; vb = tb - bCb; bCb = tb;
+            int& vr = f.qCr[c]; int tr = vr; vr = tr - bCr; bCr = tr;
+        }
+}
+
 void block_syms(const std::vector<int>& plane, int W, int H, std::vector<std::vector<Sym>>& out) {
     int bw = W / 8, bh = H / 8;
     out.assign((size_t)bw * bh, {});
@@ -398,7 +419,7 @@ void put_u16(std::vector<uint8_t>& o, int v) { o.push_back((uint8_t)(v >> 8)); o
 
 // JFIF segments, JpegSegments.hpp:55-377 as used by Image.cpp:933-972.
 void write_headers(std::vector<uint8_t>& o, int rw, int rh, const uint8_t qy[64], const uint8_t qc[64],
-                   const Table* t[4]) {
+                   const Table* t[4], int restart = 0) {
     const uint8_t soi_app0[] = {0xFF, 0xD8, 0xFF, 0xE0, 0, 16, 'J', 'F', 'I', 'F', 0, 1, 1, 0, 0, 1, 0, 1, 0, 0};
     o.insert(o.end(), soi_app0, soi_app0 + sizeof(soi_app0));
     const uint8_t* qt[2] = {qy, qc};
@@ -419,6 +440,9 @@ void write_headers(std::vector<uint8_t>& o, int rw, int rh, const uint8_t qy[64]
         for (int l = 1; l <= 16; ++l)
             for (int s : t[k]->by_len[l]) o.push_back((uint8_t)s);
     }
+    if (restart) {  // DRI, ITU T.81 B.2.4.4 (restart variant only)
+        o.push_back(0xFF); o.push_back(0xDD); put_u16(o, 4); put_u16(o, restart);
+    }
     const uint8_t sos[] = {0xFF, 0xDA, 0, 12, 3, 1, 0x00, 2, 0x11, 3, 0x11, 0, 0x3F, 0};
     o.insert(o.end(), sos, sos + sizeof(sos));
 }
@@ -432,12 +456,16 @@ void emit_block(BitWriter& bw, const std::vector<Sym>& s, const Table& dc, const
     }
 }
 
+// restart = 0: writeJPEG (Image.cpp:831-1006).  restart = R > 0: the restart-interval
+// variant — DC chains reset per interval, and after every interval but the last the
+// stream is 1-filled, stuffed and followed by RSTn (n = interval index mod 8).
 int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
-                 std::vector<uint8_t>& out) {
-    if (w <= 0 || h <= 0 || maxval <= 0 || maxval > 255) return -1;
+                 std::vector<uint8_t>& out, int restart = 0) {
+    if (w <= 0 || h <= 0 || maxval <= 0 || maxval > 255 || restart < 0 || restart > 65535) return -1;
     Frame f;
     run_to_quant(f, rgb, w, h, maxval, qy, qc);
-    dc_diff(f);
+    if (restart) dc_diff_restart(f, restart);
+    else dc_diff(f);
     std::vector<std::vector<Sym>> sY, sCb, sCr;
     block_syms(f.qY, f.W, f.H, sY);
     block_syms(f.qCb, f.sw, f.sh, sCb);
@@ -450,12 +478,19 @@ int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy
     Table tyd = build_table(ydc), tya = build_table(yac), tcd = build_table(cdc), tca = build_table(cac);
     const Table* tabs[4] = {&tyd, &tya, &tcd, &tca};
     out.clear();
-    write_headers(out, f.rw, f.rh, qy, qc, tabs);
+    write_headers(out, f.rw, f.rh, qy, qc, tabs, restart);
     // MCU interleave, Image.cpp:957-968
     BitWriter bw;
     int ybw = f.W / 8, cbw = f.sw / 8, cbh = f.sh / 8;
+    int mcu = 0;
     for (int i = 0; i < cbh; ++i)
-        for (int j = 0; j < cbw; ++j) {
+        for (int j = 0; j < cbw; ++j, ++mcu) {
+            if (restart && mcu > 0 && mcu % restart == 0) {  // end of an interval
+                bw.fill();
+                bw.stuff_into(out);
+                out.push_back(0xFF); out.push_back((uint8_t)(0xD0 + ((mcu / restart - 1) & 7)));
+                bw = BitWriter();
+            }
             emit_block(bw, sY[(size_t)(2 * i) * ybw + 2 * j], tyd, tya);
             emit_block(bw, sY[(size_t)(2 * i) * ybw + 2 * j + 1], tyd, tya);
             emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j], tyd, tya);
@@ -661,6 +696,16 @@ int64_t orc_encode_rgb(const uint8_t* rgb, int w, int h, int maxval, const uint8
                        uint8_t* out, int64_t cap) {
     std::vector<uint8_t> o;
     if (encode_frame(rgb, w, h, maxval, qy, qc, o) != 0) return -1;
+    if ((int64_t)o.size() > cap) return -(int64_t)o.size();
+    memcpy(out, o.data(), o.size());
+    return (int64_t)o.size();
+}
+
+// The restart-interval variant (restart MCUs per interval; 0 = orc_encode_rgb).
+int64_t orc_encode_rgb_restart(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                               int restart, uint8_t* out, int64_t cap) {
+    std::vector<uint8_t> o;
+    if (encode_frame(rgb, w, h, maxval, qy, qc, o, restart) != 0) return -1;
     if ((int64_t)o.size() > cap) return -(int64_t)o.size();
     memcpy(out, o.data(), o.size());
     return (int64_t)o.size();

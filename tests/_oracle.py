@@ -46,6 +46,8 @@ def orc() -> ctypes.CDLL:
         L.orc_stage_hist.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp]
         L.orc_encode_rgb.restype = i64
         L.orc_encode_rgb.argtypes = [vp, i32, i32, i32, vp, vp, vp, i64]
+        L.orc_encode_rgb_restart.restype = i64
+        L.orc_encode_rgb_restart.argtypes = [vp, i32, i32, i32, vp, vp, i32, vp, i64]
         L.orc_set_threads.argtypes = [i32]
         _orc = L
     return _orc
@@ -83,15 +85,19 @@ def huffman(text, lib=None, fn="orc_huffman"):
     return list(zip(s[:k].tolist(), ln[:k].tolist(), c[:k].tolist()))
 
 
-def encode(rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None) -> bytes:
+def encode(rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None, restart: int = 0) -> bytes:
+    """writeJPEG; restart > 0: the restart-interval variant (DRI + RSTn every `restart` MCUs)."""
     rgb = np.ascontiguousarray(rgb, np.uint8)
     h, w = rgb.shape[:2]
     if qy is None:
         qy, qc = quality_tables(quality)
-    cap = 4096 + ((w + 15) // 16) * ((h + 15) // 16) * 6 * 420
+    cap = 4096 + ((w + 15) // 16) * ((h + 15) // 16) * (6 * 420 + 4)
     out = np.empty(cap, np.uint8)
-    n = orc().orc_encode_rgb(_p(rgb), w, h, maxval, _p(np.ascontiguousarray(qy, np.uint8)),
-                             _p(np.ascontiguousarray(qc, np.uint8)), _p(out), cap)
+    qy8, qc8 = np.ascontiguousarray(qy, np.uint8), np.ascontiguousarray(qc, np.uint8)
+    if restart:
+        n = orc().orc_encode_rgb_restart(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), int(restart), _p(out), cap)
+    else:
+        n = orc().orc_encode_rgb(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), _p(out), cap)
     if n < 0:
         raise RuntimeError(f"oracle encode failed: {n}")
     return out[:n].tobytes()

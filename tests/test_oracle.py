@@ -213,3 +213,26 @@ def test_oracle_output_decodes_with_pil():
     dec = np.asarray(im.convert("RGB"), np.float64)
     psnr = 10 * np.log10(255 ** 2 / np.mean((dec - rgb) ** 2))
     assert psnr > 25
+
+
+@pytest.mark.parametrize("w,h,r", [(64, 48, 1), (200, 136, 3), (333, 211, 7), (512, 512, 32), (100, 60, 1000)])
+def test_oracle_restart_variant_decodes_to_reference_pixels(w, h, r):
+    # The restart-interval variant changes the DC prediction and
+    # the byte alignment only: DRI present, RSTn markers cycling 0..7 between the
+    # intervals, and the decoded pixels identical to the reference-mode stream's.
+    Image = pytest.importorskip("PIL.Image")
+    import io
+
+    import jpgenc_amd as J
+    rgb = J.synth_rgb8(w * 7 + h, w, h)
+    plain = _oracle.encode(rgb, 90)
+    rst = _oracle.encode(rgb, 90, restart=r)
+    nmcu = ((w + 15) // 16) * ((h + 15) // 16)
+    nint = (nmcu + r - 1) // r
+    assert rst.count(b"\xff\xdd\x00\x04") == 1
+    body = rst[rst.index(b"\xff\xda"):]
+    markers = [body[i + 1] for i in range(len(body) - 1) if body[i] == 0xFF and 0xD0 <= body[i + 1] <= 0xD7]
+    assert markers == [0xD0 + (k & 7) for k in range(nint - 1)]
+    a = np.asarray(Image.open(io.BytesIO(plain)).convert("RGB"))
+    b = np.asarray(Image.open(io.BytesIO(rst)).convert("RGB"))
+    assert np.array_equal(a, b)
