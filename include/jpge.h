@@ -168,12 +168,19 @@ void jpge_arai_constants(double a[5], double s[8]);
  *   3 jpge_stripe_code       -> summary; exchange: all-gather summaries
  *   4 jpge_stripe_pack       -> the stripe's bytes at their place in a whole-file device
  *                               buffer; then gather every [seg_off, seg_off + seg_len) to one rank.
- * Replaces nothing in the reference (single-process, single-image encoder). */
+ * With a restart interval set (jpge_set_restart_interval on every context) whose
+ * boundaries include every stripe start, the stripes are independent but for the
+ * shared tables: no DC seed is needed (phase 1's exchange can be skipped), and the
+ * summaries only carry byte lengths — the output equals the whole-image restart
+ * encode.  Replaces nothing in the reference (single-process, single-image encoder). */
 typedef struct {
-    uint64_t bits;   /* length of the stripe's bit stream */
-    uint32_t ff[8];  /* 0xFF bytes wholly inside it when it starts at bit a (mod 8) */
-    uint32_t head;   /* its first 8 bits */
-    uint32_t tail;   /* its last 8 bits */
+    uint64_t bits;    /* length of the stripe's bit stream (restart intervals: its byte length) */
+    uint32_t ff[8];   /* 0xFF bytes wholly inside it when it starts at bit a (mod 8) */
+    uint32_t head;    /* its first 8 bits */
+    uint32_t tail;    /* its last 8 bits */
+    uint32_t restart; /* 1: restart-interval stripe (every stripe starts an interval: its bytes
+                         are self-contained, so placement is a prefix sum of byte lengths) */
+    uint32_t pad;
 } jpge_stripe_summary;
 
 /* K1 on MCU rows [mcu_row0, mcu_row0 + mcu_rows) of the image; rgb = device pointer

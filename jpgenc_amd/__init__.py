@@ -57,15 +57,16 @@ class StripeSummary(ctypes.Structure):
     """jpge_stripe_summary: a stripe's bit count, inside-0xFF count per start
     alignment, first and last 8 bits."""
     _fields_ = [("bits", ctypes.c_uint64), ("ff", ctypes.c_uint32 * 8), ("head", ctypes.c_uint32),
-                ("tail", ctypes.c_uint32)]
+                ("tail", ctypes.c_uint32), ("restart", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
     def as_tuple(self):
-        return (int(self.bits), tuple(int(x) for x in self.ff), int(self.head), int(self.tail))
+        return (int(self.bits), tuple(int(x) for x in self.ff), int(self.head), int(self.tail), int(self.restart))
 
     @classmethod
     def from_tuple(cls, t):
         s = cls()
         s.bits, s.head, s.tail = t[0], t[2], t[3]
+        s.restart = t[4] if len(t) > 4 else 0
         for i in range(8):
             s.ff[i] = t[1][i]
         return s

@@ -222,6 +222,7 @@ struct Encoder::Slot {
     // stripe context (a row stripe of a larger image; whole frames: zero seeds and
     // bases, header dimensions = the frame's)
     DcSeed seed;
+    Restart rst;  // restart intervals of the frame (stripe: its first MCU in the image's numbering)
     uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
     uint32_t img_w = 0, img_h = 0;
     int tables_status = 0;
@@ -458,7 +459,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
     st.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
     st.seed = s.seed;
-    st.rst.mcus = restart_mcus_;
+    st.rst = s.rst;
     st.key_y0 = s.key_y0;
     st.key_c0 = s.key_c0;
     st.key_ncb = s.key_ncb;
@@ -485,8 +486,12 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.wgs = entropy_wgs_;
     e.diag = diag_;
     e.seed = s.seed;
-    e.rst.mcus = restart_mcus_;
-    e.seg = layout(s.g);
+    e.rst = s.rst;
+    e.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs_);
+    if (s.rst.mcus) {  // a stripe's first interval follows the previous stripes' ones
+        e.seg_index0 = s.rst.mcu0 / s.rst.mcus;
+        e.seg_markers0 = e.seg_index0 > 0 ? 1u : 0u;
+    }
     e.exp_hist = HistPtrs{};
     e.exp_cnt = nullptr;
     e.exp_key = nullptr;
@@ -531,6 +536,8 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         s.out_cap = s.cap_out;
     }
     s.seed = DcSeed();
+    s.rst = Restart();
+    s.rst.mcus = restart_mcus_;
     s.key_y0 = s.key_c0 = s.key_ncb = 0;
     s.img_w = f.width;
     s.img_h = f.height;
@@ -885,7 +892,6 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
 // lane 0's first slot and returns when its results are on the host.
 int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]) {
     JPGE_HIP(hipSetDevice(device_));
-    if (restart_mcus_) return kErrArg;  // (the stripe phases run the reference's single interval)
     if (!d.rgb || !last_dc || d.width == 0 || d.height == 0 || d.width > 65535 || d.height > 65535) return kErrArg;
     if (d.maxval < 1 || d.maxval > 255) return kErrRange;
     const uint32_t mh_img = (d.height + 15) / 16;
@@ -896,6 +902,8 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
         if (!qy[i] || !qc[i]) return kErrArg;
     const uint32_t hs = std::min(16 * d.mcu_rows, d.height - 16 * d.mcu_row0);
     const Geometry g = geometry(d.width, hs);
+    // restart intervals: the stripe must start one (its bytes are then its own)
+    if (restart_mcus_ && ((uint64_t)d.mcu_row0 * g.mw) % restart_mcus_ != 0) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (const int st = ensure(s, g, 0, 0)) return st;
     std::memcpy(s.qy, qy, 64);
@@ -906,6 +914,9 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
     s.img_w = d.width;
     s.img_h = d.height;
     s.seed = DcSeed();
+    s.rst = Restart();
+    s.rst.mcus = restart_mcus_;
+    s.rst.mcu0 = d.mcu_row0 * g.mw;
     s.key_y0 = 2ull * d.mcu_row0 * (2ull * g.mw);  // Y blocks above the stripe (raster)
     s.key_c0 = (uint64_t)d.mcu_row0 * g.mw;         // Cb blocks above it
     s.key_ncb = (uint64_t)mh_img * g.mw;            // Cb blocks of the image
@@ -922,7 +933,6 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
 
 int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t first[1024]) {
     JPGE_HIP(hipSetDevice(device_));
-    if (restart_mcus_) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !seed || !counts || !first) return kErrArg;
     for (int c = 0; c < 3; ++c) s.seed.v[c] = seed[c];
@@ -943,7 +953,6 @@ int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t
 int Encoder::stripe_code(const uint32_t counts[1024], const uint64_t first[1024], StripeSummary* sum,
                          size_t* hdr_len) {
     JPGE_HIP(hipSetDevice(device_));
-    if (restart_mcus_) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !counts || !first || !sum) return kErrArg;
     s.out_dev = nullptr;
@@ -970,6 +979,21 @@ uint32_t fill_bits(uint32_t eb, uint32_t tail) {  // Bitstream::fill, BitstreamG
 int Encoder::stripe_place(const StripeSummary* all, int n, int index, size_t hdr_len, uint64_t* p_ext,
                           uint64_t* q_ext, uint32_t* head_split, size_t* seg_off, size_t* total_len) {
     if (!all || n <= 0 || index < 0 || index >= n) return kErrArg;
+    if (all[0].restart) {  // restart stripes: self-contained byte runs, one after another
+        uint64_t base = 0;
+        for (int r = 0; r < n; ++r) {
+            if (!all[r].restart) return kErrArg;
+            if (r == index) {
+                if (p_ext) *p_ext = 0;
+                if (q_ext) *q_ext = base;  // (the byte base of the stripe after the header)
+                if (head_split) *head_split = 0;
+                if (seg_off) *seg_off = r == 0 ? 0 : hdr_len + (size_t)base;
+            }
+            base += all[r].bits;
+        }
+        if (total_len) *total_len = hdr_len + (size_t)base + 2;
+        return kOk;
+    }
     uint64_t p = 0, q = 0;
     for (int r = 0; r < n; ++r) {
         if (all[r].bits < 8) return kErrArg;  // (a stripe codes >= 2 bits per block, 6 blocks per MCU)
@@ -994,7 +1018,6 @@ int Encoder::stripe_place(const StripeSummary* all, int n, int index, size_t hdr
 int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* out_dev, size_t cap, size_t* seg_off,
                          size_t* seg_len, size_t* total_len) {
     JPGE_HIP(hipSetDevice(device_));
-    if (restart_mcus_) return kErrArg;
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !out_dev || !s.hdr_len) return kErrArg;
     uint64_t p_ext = 0, q_ext = 0;
@@ -1007,9 +1030,13 @@ int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* ou
     s.seq = ++seq_counter_;
     s.h_result[2] = 0;
     EntropyArgs e = entropy_args(s);
-    e.p_ext = p_ext;
-    e.q_ext = q_ext;
-    e.head_split = head;
+    if (s.rst.mcus) {
+        e.out_base = q_ext;  // (placed in phase 3, relative to the stripe's start)
+    } else {
+        e.p_ext = p_ext;
+        e.q_ext = q_ext;
+        e.head_split = head;
+    }
     e.flags = (index == 0 ? kStripeFirst : 0u) | (index == n - 1 ? kStripeLast : 0u) | kExtPlace;
     JPGE_HIP(launch_entropy_place_pack(e, s.stream));
     if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream)) return w;

@@ -424,6 +424,12 @@ __device__ void place_restart(const EntropyArgs& a, const RecView& R, uint32_t* 
         }
         p = (p + 7) & ~7ull;
     }
+    if (a.summary && s0 < s1 && s1 == L.nseg) {  // the frame's (stripe's) entropy byte length
+        StripeSummary sm{};
+        sm.bits = (p >> 3) + (q - a.q_ext) + 2ull * (L.nseg - 1 + a.seg_markers0);
+        sm.restart = 1;
+        *a.summary = sm;
+    }
 }
 
 // entropy_scan_kernel — one workgroup over all G records.  Place mode: every
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(kScanThreads) void entropy_scan_kernel(EntropyArgs 
     }
     __syncthreads();
     if (tid == 0) {
-        StripeSummary sm;
+        StripeSummary sm{};
         sm.bits = total;
 #pragma unroll
         for (int al = 0; al < 8; ++al) sm.ff[al] = tot8[al];
@@ -542,12 +548,12 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
     const uint32_t eb = (b + Lb) & 7;   // bits in the byte after them
     const uint32_t n_own = nc + ((fills && eb) ? 1u : 0u);
     const uint32_t markers = a.rst.mcus ? S.seg + a.seg_markers0 : 0u;  // RST markers before this segment
-    const uint64_t D0 = a.hdr_len + (P >> 3) + S.Q + 2ull * markers;
+    const uint64_t D0 = a.hdr_len + a.out_base + (P >> 3) + S.Q + 2ull * markers;
     const uint64_t ntot = (uint64_t)n_own + ftotal + (eoi ? 2u : 0u);
     const bool fits = D0 + ntot <= a.out_cap;
     if (fits && wt.first && markers && tid == 0) {  // RSTn ahead of the segment (not stuffed)
         a.out[D0 - 2] = 0xFF;
-        a.out[D0 - 1] = (uint8_t)(0xD0 + ((markers - 1) & 7));
+        a.out[D0 - 1] = (uint8_t)(0xD0 + ((a.seg_index0 + S.seg - 1) & 7));  // RST(interval - 1 mod 8)
     }
     const uint32_t split = S.split, fill = S.fill;
     const uint32_t* R32 = reinterpret_cast<const uint32_t*>(a.ubuf + (uint64_t)wg * kEntropyRegionBytes);
@@ -696,7 +702,9 @@ hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, a, G, 1);
+    // (restart intervals: the stripe's placement is its own, computed now; its summary
+    // is its byte length)
+    hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, a, G, a.rst.mcus ? 0 : 1);
     return hipGetLastError();
 }
 
@@ -705,9 +713,11 @@ hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s) {
     if (!a.place) return hipErrorInvalidValue;
     EntropyArgs b = a;
     b.flags |= kExtPlace;
-    hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (!a.rst.mcus) {  // (restart intervals: placed by launch_entropy_code_summary)
+        hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
     return hipGetLastError();
 }

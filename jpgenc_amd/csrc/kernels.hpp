@@ -145,11 +145,13 @@ struct alignas(16) WgPlace {
 // A stripe's entropy summary (entropy_scan_kernel, summary mode): enough for the
 // stripes to place their bytes after one all-gather.
 struct StripeSummary {
-    uint64_t bits;   // length of the stripe's stream
+    uint64_t bits;   // length of the stripe's stream (restart intervals: its bytes, markers and fills included)
     uint32_t ff[8];  // ff[a]: 0xFF bytes wholly inside the stripe when it starts at bit a (mod 8),
                      // the byte shared with the previous stripe and the final fill byte excluded
     uint32_t head;   // its first 8 bits (MSB-first byte)
     uint32_t tail;   // its last 8 bits
+    uint32_t restart;  // 1: restart-interval stripe (byte-aligned; bits = byte length)
+    uint32_t pad;
 };
 
 constexpr uint32_t kStripeFirst = 1u;  // holds the image's first bit: writes the headers
@@ -187,7 +189,9 @@ struct EntropyArgs {
     StripeSummary* summary = nullptr;  // summary mode output
     Restart rst;                       // restart intervals (rst.mcus = 0: none)
     SegLayout seg;                     // workgroup partition (host: seg_layout)
-    uint32_t seg_markers0 = 0;         // RST markers before the frame's first segment (stripes)
+    uint32_t seg_markers0 = 0;         // RST markers in this output before the frame's first segment (stripes)
+    uint32_t seg_index0 = 0;           // the image's interval index of the frame's first segment (stripes)
+    uint64_t out_base = 0;             // restart stripes: bytes of earlier stripes after the header
     uint64_t* dbg;
 };
 

@@ -24,17 +24,30 @@ import numpy as np
 import jpgenc_amd as J
 
 
-def stripe_rows(mcu_rows: int, n: int) -> list[tuple[int, int]]:
-    """Split mcu_rows MCU rows into n contiguous stripes (first rows0, count), as even as possible."""
-    if n < 1 or n > mcu_rows:
-        raise ValueError(f"cannot cut {mcu_rows} MCU rows into {n} stripes")
-    base, extra = divmod(mcu_rows, n)
-    out, r0 = [], 0
+def stripe_rows(mcu_rows: int, n: int, align: int = 1) -> list[tuple[int, int]]:
+    """Split mcu_rows MCU rows into n contiguous stripes (first rows0, count), as even as
+    possible, every stripe starting at a multiple of `align` rows."""
+    units = (mcu_rows + align - 1) // align
+    if n < 1 or n > units:
+        raise ValueError(f"cannot cut {mcu_rows} MCU rows into {n} stripes of whole {align}-row units")
+    base, extra = divmod(units, n)
+    out, u0 = [], 0
     for r in range(n):
         c = base + (1 if r < extra else 0)
-        out.append((r0, c))
-        r0 += c
+        r0 = u0 * align
+        out.append((r0, min(mcu_rows, (u0 + c) * align) - r0))
+        u0 += c
     return out
+
+
+def restart_align(width: int, restart: int) -> int:
+    """MCU rows between possible stripe starts when every stripe must begin a restart
+    interval of `restart` MCUs (1 without restart intervals)."""
+    import math
+    if not restart:
+        return 1
+    mw = (width + 15) // 16
+    return restart // math.gcd(restart, mw)
 
 
 def combine_stats(all_counts: list[np.ndarray], all_first: list[np.ndarray]) -> tuple[np.ndarray, np.ndarray]:
@@ -50,11 +63,11 @@ def seeds_from(last_dcs: list[np.ndarray], r: int) -> np.ndarray:
 
 
 def encode_stripes_local(encoders: list, stripes_rgb: list[tuple[int, int]], width: int, height: int,
-                         quality: int, out_ptr: int, cap: int, maxval: int = 255) -> int:
+                         quality: int, out_ptr: int, cap: int, maxval: int = 255, rows=None) -> int:
     """All stripes in one process: encoders[r] encodes stripe r (device RGB pointer, stride);
     every stripe writes into the same whole-file device buffer out_ptr.  Returns the length."""
     n = len(encoders)
-    rows = stripe_rows((height + 15) // 16, n)
+    rows = rows or stripe_rows((height + 15) // 16, n)
     last = [encoders[r].stripe_transform(stripes_rgb[r][0], stripes_rgb[r][1], width, height, rows[r][0],
                                          rows[r][1], quality, maxval) for r in range(n)]
     stats = [encoders[r].stripe_stats(seeds_from(last, r)) for r in range(n)]
@@ -68,24 +81,30 @@ def encode_stripes_local(encoders: list, stripes_rgb: list[tuple[int, int]], wid
 
 
 def encode_stripe_dist(enc, rgb_ptr: int, stride: int, width: int, height: int, quality: int, out, maxval: int = 255,
-                       group=None) -> int:
+                       group=None, restart: int = 0) -> int:
     """This rank's stripe of a torch.distributed job (rank r of world n takes stripe r).
     rgb_ptr: device RGB of the stripe's rows (stripe_rows() says which); out: a uint8
     torch tensor on this rank's device with whole-file capacity.  After the call rank
-    0's `out` holds the whole file; returns its length (every rank)."""
+    0's `out` holds the whole file; returns its length (every rank).  restart: the
+    encoder's restart interval (enc.set_restart), whose boundaries include every
+    stripe start — then there is no DC seed exchange and the summaries only place
+    byte runs (the RCCL traffic is the histogram all-reduce and the segment gather)."""
     import torch
     import torch.distributed as dist
 
     rank, n = dist.get_rank(group), dist.get_world_size(group)
-    rows = stripe_rows((height + 15) // 16, n)
+    rows = stripe_rows((height + 15) // 16, n, restart_align(width, restart))
     # exchanges in device memory over RCCL; through host memory for gloo (CPU tests,
     # several ranks sharing one GPU)
     dev = out.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
     last = enc.stripe_transform(rgb_ptr, stride, width, height, rows[rank][0], rows[rank][1], quality, maxval)
-    # 1) DC seeds: all-gather of 3 x int32 per rank
-    g = [torch.zeros(3, dtype=torch.int32, device=dev) for _ in range(n)]
-    dist.all_gather(g, torch.from_numpy(last).to(dev), group=group)
-    seed = seeds_from([t.cpu().numpy() for t in g], rank)
+    if restart:  # every stripe starts a restart interval: its DC chain starts at 0
+        seed = np.zeros(3, np.int32)
+    else:
+        # 1) DC seeds: all-gather of 3 x int32 per rank
+        g = [torch.zeros(3, dtype=torch.int32, device=dev) for _ in range(n)]
+        dist.all_gather(g, torch.from_numpy(last).to(dev), group=group)
+        seed = seeds_from([t.cpu().numpy() for t in g], rank)
     counts, first = enc.stripe_stats(seed)
     # 2) histograms: sum of counts, minimum of first-occurrence keys (int64 view: keys < 2^63)
     tc = torch.from_numpy(counts.astype(np.int64)).to(dev)
@@ -96,14 +115,16 @@ def encode_stripe_dist(enc, rgb_ptr: int, stride: int, width: int, height: int, 
     fk = tf.cpu().numpy().astype(np.uint64)
     first = np.where(counts > 0, fk, np.uint64(2**64 - 1))
     summary, hdr_len = enc.stripe_code(counts, first)
-    # 3) summaries: all-gather of 11 x int64 per rank (bits, ff[8], head, tail)
-    mine = torch.tensor([summary[0], *summary[1], summary[2], summary[3]], dtype=torch.int64, device=dev)
-    gs = [torch.zeros(11, dtype=torch.int64, device=dev) for _ in range(n)]
+    # 3) summaries: all-gather of 12 x int64 per rank (bits, ff[8], head, tail, restart);
+    #    with restart intervals only the byte lengths matter (stitching the segments)
+    mine = torch.tensor([summary[0], *summary[1], summary[2], summary[3], summary[4]], dtype=torch.int64,
+                        device=dev)
+    gs = [torch.zeros(12, dtype=torch.int64, device=dev) for _ in range(n)]
     dist.all_gather(gs, mine, group=group)
     summaries = []
     for t in gs:
         v = [int(x) for x in t.cpu().tolist()]
-        summaries.append((v[0], tuple(v[1:9]), v[9], v[10]))
+        summaries.append((v[0], tuple(v[1:9]), v[9], v[10], v[11]))
     off, ln, total = enc.stripe_pack(summaries, rank, out.data_ptr(), out.numel())
     # 4) segments to rank 0 (point-to-point)
     spans = [J.stripe_place(summaries, r, hdr_len) for r in range(n)]

@@ -31,8 +31,8 @@ def _byte(bits):
 
 
 def _summary(bits):
-    """(bits, ff[a], head, tail) as the GPU computes it: 0xFF bytes wholly inside
-    the stripe when it starts at bit a (mod 8)."""
+    """(bits, ff[a], head, tail, restart=0) as the GPU computes it: 0xFF bytes wholly
+    inside the stripe when it starts at bit a (mod 8)."""
     L = len(bits)
     ff = []
     for a in range(8):
@@ -42,7 +42,7 @@ def _summary(bits):
             c += all(bits[s:s + 8])
             s += 8
         ff.append(c)
-    return (L, tuple(ff), _byte(bits[:8]), _byte(bits[-8:]))
+    return (L, tuple(ff), _byte(bits[:8]), _byte(bits[-8:]), 0)
 
 
 def _file(streams, hdr):
