@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--workload", choices=["4k-frames", "16k-striped"], default="4k-frames",
                     help="4k-frames: the BASELINE metric (frames sharded over ranks); 16k-striped: one "
                          "16384x16384 frame per step, row-striped over the ranks (SURVEY 8(e) config 5)")
+    ap.add_argument("--restart", type=int, default=None,
+                    help="restart interval in MCUs (16k-striped: default 1024 = one interval per MCU row, "
+                         "the config's 'tiled with restart intervals'; 0 = the reference's single interval)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
@@ -187,11 +190,13 @@ def run_striped16k(args, rank, local, world, pg):
 
     torch.cuda.set_device(local)
     W = H = 16384
+    restart = 1024 if args.restart is None else args.restart
     rgb = J.synth_rgb8(5, W, H)  # SURVEY 8(d) config 5 seed
     cap = J.max_jpeg_bytes(W, H)
     out = torch.empty(cap, dtype=torch.uint8, device=f"cuda:{local}")
     if world == 1:
         enc = J.Encoder(local)
+        enc.set_restart(restart)
         src = torch.from_numpy(rgb.reshape(-1)).to(f"cuda:{local}")
         del rgb
 
@@ -202,13 +207,15 @@ def run_striped16k(args, rank, local, world, pg):
         import torch.distributed as dist
 
         rccl = dist.new_group(backend="nccl")  # the exchanges and the gather ride RCCL over xGMI
-        r0, nr = stripes.stripe_rows(H // 16, world)[rank]
+        r0, nr = stripes.stripe_rows(H // 16, world, stripes.restart_align(W, restart))[rank]
         src = torch.from_numpy(np.ascontiguousarray(rgb[16 * r0:16 * (r0 + nr)]).reshape(-1)).to(f"cuda:{local}")
         del rgb
         enc = J.Encoder(local, lanes=1)
+        enc.set_restart(restart)
 
         def step():
-            return stripes.encode_stripe_dist(enc, src.data_ptr(), W * 3, W, H, args.quality, out, group=rccl)
+            return stripes.encode_stripe_dist(enc, src.data_ptr(), W * 3, W, H, args.quality, out, group=rccl,
+                                              restart=restart)
     for _ in range(args.warmup):
         n = step()
     torch.cuda.synchronize()
@@ -227,10 +234,13 @@ def run_striped16k(args, rank, local, world, pg):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 photo-like frame, seed 5, HBM-resident)",
             "config": {"workload": f"16384x16384 4:2:0 Q{args.quality}, one frame per step, "
+                                   + (f"restart interval {restart} MCUs, " if restart else "single interval, ")
                                    + ("whole frame on one GPU" if world == 1 else
-                                      f"row-striped over {world} GPUs (RCCL: DC seeds, histogram sum/min, "
-                                      f"summaries; segments gathered to rank 0)"),
-                       "jpeg_bytes": int(n)},
+                                      f"row-striped over {world} GPUs (RCCL: "
+                                      + ("histogram sum/min, segment lengths; segments gathered to rank 0)"
+                                         if restart else
+                                         "DC seeds, histogram sum/min, summaries; segments gathered to rank 0)")),
+                       "restart_mcus": restart, "jpeg_bytes": int(n)},
         }), flush=True)
     enc.close()
 
