@@ -51,9 +51,10 @@ def parse():
     ap.add_argument("--solo-batches", type=int, default=2,
                     help="batches through a 1-lane encoder after the timed region (kernel times alone; 0 = skip)")
     ap.add_argument("--lanes", type=int, default=0, help="encoder lanes (0 = library default)")
-    ap.add_argument("--workload", choices=["4k-frames", "16k-striped"], default="4k-frames",
+    ap.add_argument("--workload", choices=["4k-frames", "16k-striped", "ppm-files"], default="4k-frames",
                     help="4k-frames: the BASELINE metric (frames sharded over ranks); 16k-striped: one "
-                         "16384x16384 frame per step, row-striped over the ranks (SURVEY 8(e) config 5)")
+                         "16384x16384 frame per step, row-striped over the ranks (SURVEY 8(e) config 5); "
+                         "ppm-files: PPM files -> .jpg files through the ingest pipeline (PCIe-inclusive)")
     ap.add_argument("--restart", type=int, default=None,
                     help="restart interval in MCUs (16k-striped: default 1024 = one interval per MCU row, "
                          "the config's 'tiled with restart intervals'; 0 = the reference's single interval)")
@@ -245,9 +246,66 @@ def run_striped16k(args, rank, local, world, pg):
     enc.close()
 
 
+def run_ppm_files(args, rank, local, world, pg):
+    """F synthetic P6 files (in /dev/shm, i.e. the page cache) ->
+    .jpg files per step through jpge_encode_files: file read + parse into pinned
+    memory, H2D, kernels, D2H and file write all inside the timed step."""
+    import shutil
+    import tempfile
+
+    import torch
+
+    import jpgenc_amd as J
+
+    torch.cuda.set_device(local)
+    W, H, F = args.width, args.height, args.frames
+    tmp = tempfile.mkdtemp(prefix=f"jpge_ppm_{rank}_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        ins, outs = [], []
+        for i in range(F):
+            p = os.path.join(tmp, f"f{i}.ppm")
+            with open(p, "wb") as f:
+                f.write(f"P6\n{W} {H}\n255\n".encode())
+                f.write(J.synth_rgb8(frame_seed(rank, i), W, H).tobytes())
+            ins.append(p)
+            outs.append(os.path.join(tmp, f"f{i}.jpg"))
+        enc = J.Encoder(local)
+        for _ in range(args.warmup):
+            enc.encode_files(ins, outs, quality=args.quality)
+        barrier(pg)
+        t0 = time.perf_counter()
+        nbytes = 0
+        for _ in range(args.steps):
+            nbytes += sum(enc.encode_files(ins, outs, quality=args.quality))
+        barrier(pg)
+        dt = max_over_ranks(pg, time.perf_counter() - t0)
+        pixels = sum_over_ranks(pg, float(W * H * F * args.steps))
+        if rank == 0:
+            print(json.dumps({
+                "metric": f"MPixels/s encode from PPM files ({W}x{H} 4:2:0 Q={args.quality})",
+                "value": round(pixels / dt / 1e6, 1), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic P6 files (deterministic splitmix64 photo-like frames) in /dev/shm",
+                "config": {"workload": f"{F} PPM files -> .jpg files per GPU per step (jpge_encode_files: read + "
+                                       f"parse into pinned memory, H2D, kernels, D2H, write)",
+                           "width": W, "height": H, "quality": args.quality, "files_per_step_per_gpu": F,
+                           "avg_jpeg_bytes": int(nbytes / (args.steps * F)),
+                           "parallelism": f"files sharded over {world} GPU(s)"},
+            }), flush=True)
+        enc.close()
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     args = parse()
     rank, local, world, pg = dist_setup(args.gpus)
+    if args.workload == "ppm-files":
+        run_ppm_files(args, rank, local, world, pg)
+        if pg is not None:
+            pg.destroy_process_group()
+        return
     if args.workload == "16k-striped":
         run_striped16k(args, rank, local, world, pg)
         if pg is not None:

@@ -148,6 +148,15 @@ int jpge_ppm_info(const uint8_t* buf, size_t n, uint32_t* width, uint32_t* heigh
 /* Convenience: PPM file -> .jpg file at the given quality (the CLI path, main.cpp:8-32). */
 int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, int quality);
 
+/* Many PPM files -> .jpg files (the CLI path over a list), pipelined: worker threads
+ * read and parse each file into pinned memory while the previous group of frames is
+ * encoded (H2D queued ahead of the kernels on each lane) and the one before is copied
+ * back and written.  lens/statuses (optional, n entries) get each file's .jpg length
+ * and jpge_status; returns the first failing status.  group = frames per stage
+ * (0 = 8, at most 64).  Bytes equal jpge_encode_file's for every file. */
+int jpge_encode_files(jpge_ctx* ctx, const char* const* ppm_paths, const char* const* jpg_paths, int n, int quality,
+                      size_t* lens, int* statuses, int group);
+
 /* Deterministic synthetic frame (kind 0 photo-like, 1 random bytes, 2 flat). */
 int jpge_synth_rgb8(uint64_t seed, uint32_t width, uint32_t height, int kind, uint8_t* out, size_t stride);
 

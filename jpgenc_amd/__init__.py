@@ -33,7 +33,7 @@ EXPORTS = (
     "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_open_ex", "jpge_close", "jpge_set_timing",
     "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_set_restart_interval", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
-    "jpge_ppm_info", "jpge_encode_file", "jpge_synth_rgb8", "jpge_arai_constants",
+    "jpge_ppm_info", "jpge_encode_file", "jpge_encode_files", "jpge_synth_rgb8", "jpge_arai_constants",
     "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
 )
 
@@ -120,6 +120,8 @@ def lib() -> ctypes.CDLL:
                                      ctypes.POINTER(i32)]
         L.jpge_ppm_info.argtypes = [vp, sz, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(i32)]
         L.jpge_encode_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, i32]
+        L.jpge_encode_files.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), i32,
+                                        i32, vp, vp, i32]
         L.jpge_synth_rgb8.argtypes = [ctypes.c_uint64, u32, u32, i32, vp, sz]
         L.jpge_arai_constants.argtypes = [vp, vp]
         L.jpge_arai_constants.restype = None
@@ -378,6 +380,23 @@ class Encoder:
         _check(lib().jpge_stripe_pack(self._ctx, arr, len(summaries), index, out_ptr, cap, ctypes.byref(off),
                                       ctypes.byref(ln), ctypes.byref(tot)), "stripe_pack")
         return off.value, ln.value, tot.value
+
+    def encode_file(self, ppm_path: str, jpg_path: str, quality: int = 50) -> None:
+        """main.cpp: loadPPM(ppm_path) + writeJPEG(jpg_path)."""
+        _check(lib().jpge_encode_file(self._ctx, ppm_path.encode(), jpg_path.encode(), int(quality)), "encode_file")
+
+    def encode_files(self, ppm_paths: list[str], jpg_paths: list[str], quality: int = 50, group: int = 0):
+        """Many PPM files -> .jpg files through the ingest pipeline; returns the .jpg lengths."""
+        n = len(ppm_paths)
+        if len(jpg_paths) != n:
+            raise ValueError("ppm_paths and jpg_paths differ in length")
+        ins = (ctypes.c_char_p * n)(*[p.encode() for p in ppm_paths])
+        outs = (ctypes.c_char_p * n)(*[p.encode() for p in jpg_paths])
+        lens = np.zeros(n, np.uint64)
+        sts = np.zeros(n, np.int32)
+        st = lib().jpge_encode_files(self._ctx, ins, outs, n, int(quality), _p(lens), _p(sts), int(group))
+        _check(st, f"encode_files (statuses {sts.tolist()})" if st else "encode_files")
+        return [int(x) for x in lens]
 
     def symbol_stats(self, rgb: np.ndarray, quality: int = 50, maxval: int = 255):
         rgb = np.ascontiguousarray(rgb, np.uint8)

@@ -11,9 +11,11 @@
 #include "encoder.hpp"
 #include "host_io.hpp"
 #include "huffman.hpp"
+#include "ingest.hpp"
 
 struct jpge_ctx {
     std::unique_ptr<jpge::Encoder> enc;
+    std::unique_ptr<jpge::IngestBuffers, jpge::IngestBuffersDeleter> ingest;  // jpge_encode_files' buffers
 };
 
 namespace {
@@ -231,6 +233,12 @@ int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, 
     if (!f.is_open()) return JPGE_E_IO;
     f.write(reinterpret_cast<const char*>(out.data()), (std::streamsize)len);
     return f.good() ? JPGE_OK : JPGE_E_IO;
+}
+
+int jpge_encode_files(jpge_ctx* ctx, const char* const* ppm_paths, const char* const* jpg_paths, int n, int quality,
+                      size_t* lens, int* statuses, int group) {
+    if (!ctx) return JPGE_E_ARG;
+    return jpge::encode_files(*ctx->enc, ctx->ingest, ppm_paths, jpg_paths, n, quality, lens, statuses, group);
 }
 
 int jpge_synth_rgb8(uint64_t seed, uint32_t w, uint32_t h, int kind, uint8_t* out, size_t stride) {

@@ -524,7 +524,10 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         s.in_dev = f.rgb;
         s.in_stride = stride;
     } else {
-        JPGE_HIP(hipMemcpy2DAsync(s.d_in, dev_pitch, f.rgb, stride, row, f.height, hipMemcpyHostToDevice, s.stream));
+        if (stride == dev_pitch)  // one linear copy (a 2D copy can fall back to a slower engine path)
+            JPGE_HIP(hipMemcpyAsync(s.d_in, f.rgb, dev_pitch * f.height, hipMemcpyHostToDevice, s.stream));
+        else
+            JPGE_HIP(hipMemcpy2DAsync(s.d_in, dev_pitch, f.rgb, stride, row, f.height, hipMemcpyHostToDevice, s.stream));
         s.in_dev = s.d_in;
         s.in_stride = dev_pitch;
     }

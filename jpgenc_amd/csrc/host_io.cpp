@@ -121,6 +121,40 @@ int parse_ppm(const uint8_t* buf, size_t n, PpmImage& out) {
     return kOk;
 }
 
+int parse_ppm_inplace(uint8_t* buf, size_t n, uint32_t& width, uint32_t& height, int& maxval, size_t& offset) {
+    Tokens t(buf, n);
+    std::string magic = t.word();
+    if (magic != "P3" && magic != "P6") return kErrFormat;
+    long w = 0, h = 0, mv = 0;
+    if (!to_int(t.word(), w) || !to_int(t.word(), h) || !to_int(t.word(), mv)) return kErrFormat;
+    if (w <= 0 || h <= 0 || w > 65535 || h > 65535) return kErrFormat;
+    if (mv < 1 || mv > 255) return kErrRange;
+    width = (uint32_t)w;
+    height = (uint32_t)h;
+    maxval = (int)mv;
+    const size_t cnt = (size_t)w * (size_t)h * 3;
+    if (magic == "P6") {  // loadP6PPM, Image.cpp:411-418: the samples are the frame
+        if (t.pos() + cnt > n) return kErrTruncated;
+        offset = t.pos();
+        if (mv < 255)
+            for (size_t i = 0; i < cnt; ++i)
+                if (buf[offset + i] > mv) return kErrRange;
+        return kOk;
+    }
+    // loadP3PPM, Image.cpp:393-408: sample i is written over the text at byte i, which
+    // the tokenizer has passed (every earlier sample took >= 2 characters)
+    for (size_t i = 0; i < cnt; ++i) {
+        std::string wd = t.word();
+        if (wd.empty() && t.pos() >= n) return kErrTruncated;
+        long v = 0;
+        for (char c : wd) v = v * 10 + (c - '0');
+        if (v < 0 || v > mv) return kErrRange;
+        buf[i] = (uint8_t)v;
+    }
+    offset = 0;
+    return kOk;
+}
+
 int load_ppm_file(const std::string& path, PpmImage& out) {
     std::ifstream f(path, std::ios::binary);
     if (!f.is_open()) return kErrIo;

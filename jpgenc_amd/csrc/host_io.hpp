@@ -41,6 +41,9 @@ struct PpmImage {
 // maxval or maxval outside 1..255 -> kErrRange.
 int parse_ppm(const uint8_t* buf, size_t n, PpmImage& out);
 int load_ppm_file(const std::string& path, PpmImage& out);
+// The same parse without a copy: P6 -> offset of the samples in buf; P3 -> the
+// samples written over the text at buf[0..) (offset 0).
+int parse_ppm_inplace(uint8_t* buf, size_t n, uint32_t& width, uint32_t& height, int& maxval, size_t& offset);
 
 // Annex K tables (Image.cpp:850-869) scaled for quality 1..100 with the IJG rule
 // (50 == the reference's tables unchanged).

@@ -208,3 +208,54 @@ def test_facade_cli_roundtrip(tmp_path):
     assert "Processing image size: 26x19" in r.stdout and "Encoding duration:" in r.stdout
     img = J.load_ppm(src)
     assert out.read_bytes() == _oracle.encode(img.rgb, 50, img.maxval)
+
+
+def _write_ppm(path, rgb, maxval=255, ascii=False):
+    h, w = rgb.shape[:2]
+    if ascii:
+        body = "\n".join(" ".join(str(int(v)) for v in row.reshape(-1)) for row in rgb) + "\n"
+        data = f"P3\n# jpge test\n{w} {h}\n{maxval}\n".encode() + body.encode()
+    else:
+        data = f"P6\n{w} {h}\n{maxval}\n".encode() + np.ascontiguousarray(rgb, np.uint8).tobytes()
+    with open(path, "wb") as f:
+        f.write(data)
+
+
+# the PPM ingest pipeline (read + parse into pinned memory, H2D
+# queued ahead of the kernels, D2H + write) — every file's bytes must be the
+# oracle's, across group boundaries and with P3/P6 and maxval < 255 mixed.
+@pytest.mark.parametrize("group", [0, 3])
+def test_encode_files_pipeline(encoder, tmp_path, group):
+    ins, outs, want = [], [], []
+    for i, path in enumerate(_ppm_files()):
+        img = J.load_ppm(path)
+        ins.append(path)
+        outs.append(str(tmp_path / f"ref{i}.jpg"))
+        want.append(_oracle.encode(img.rgb, 90, img.maxval))
+    for i, (w, h, mv, asc) in enumerate([(640, 480, 255, False), (333, 211, 255, True), (1920, 1080, 255, False),
+                                         (100, 60, 100, False), (64, 48, 15, True)]):
+        rgb = _scaled(J.synth_rgb8(600 + i, w, h), mv)
+        p = str(tmp_path / f"s{i}.ppm")
+        _write_ppm(p, rgb, mv, asc)
+        ins.append(p)
+        outs.append(str(tmp_path / f"s{i}.jpg"))
+        want.append(_oracle.encode(rgb, 90, mv))
+    lens = encoder.encode_files(ins, outs, quality=90, group=group)
+    for o, wnt, n in zip(outs, want, lens):
+        with open(o, "rb") as f:
+            assert f.read() == wnt
+        assert n == len(wnt)
+
+
+def test_encode_files_reports_bad_file(encoder, tmp_path):
+    good = str(tmp_path / "g.ppm")
+    _write_ppm(good, J.synth_rgb8(1, 32, 32))
+    bad = str(tmp_path / "b.ppm")
+    with open(bad, "wb") as f:
+        f.write(b"P5\n2 2\n255\n....")
+    with pytest.raises(J.JpgeError) as e:
+        encoder.encode_files([good, bad, str(tmp_path / "missing.ppm")],
+                             [str(tmp_path / "g.jpg"), str(tmp_path / "b.jpg"), str(tmp_path / "m.jpg")], quality=50)
+    assert "[0, 5, 6]" in str(e.value)
+    with open(str(tmp_path / "g.jpg"), "rb") as f:
+        assert f.read() == _oracle.encode(J.synth_rgb8(1, 32, 32), 50)
