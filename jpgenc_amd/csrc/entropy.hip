@@ -177,6 +177,20 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     regs.init(tid);
     regs.load(a.coef, tile_b0(0), tile_nb(0), tid);
     uint32_t wl = 0;  // workgroup-local bit position of the current tile
+    // 0xFF bytes of the stream at each byte alignment, counted on the stage words as
+    // they are stored (see the note after the loop).  A word's count needs the next
+    // word's first 7 bits: the last complete word of a tile waits (thread 0's `pend`)
+    // until the next tile has completed the word after it.
+    uint32_t c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto count_word = [&](uint32_t x, uint32_t nx) {
+        uint32_t y = x;  // bit 31-t: stream bits [32m+t, 32m+t+8) are all ones
+#pragma unroll
+        for (int k = 1; k < 8; ++k) y &= __builtin_amdgcn_alignbit(x, nx, 32 - k);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c8[(8 - r) & 7] += __builtin_popcount(y & (0x80808080u >> r));
+    };
+    uint32_t pend = 0;
+    bool has_pend = false;
     uint64_t tq = JPGE_NOW();
     for (int lt = 0; lt < ntl; ++lt) {
         const uint64_t b0 = tile_b0(lt);
@@ -221,8 +235,15 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
             uint32_t v = L.u.stage[w];
             if (w == 0) v |= L.carry;  // partial last word of the previous tile
             R32[wbase + w] = __builtin_bswap32(v);
+            if (w + 1 < ncw) count_word(v, L.u.stage[w + 1]);
         }
         if (tid == 0) {  // (thread 0 consumed the old carry above)
+            if (ncw) {
+                const uint32_t w0 = L.u.stage[0] | L.carry;
+                if (has_pend) count_word(pend, w0);
+                pend = ncw == 1 ? w0 : L.u.stage[ncw - 1];
+                has_pend = true;
+            }
             uint32_t v = L.u.stage[ncw];
             if (ncw == 0) v |= L.carry;
             L.carry = v;
@@ -239,23 +260,17 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     // ---- 0xFF bytes of the stream at each byte alignment b ----
     // Starting at global bit offset P (b = P & 7), output byte j of this workgroup
     // holds local bits [8j - b, 8j - b + 8): it is 0xFF iff 8 one-bits start at
-    // s = 8j - b.  Mark every run start (y), count the starts with s = -b (mod 8).
-    // Starts s < 0 (the byte split with the predecessor) do not exist and runs past
-    // Lb meet the zero padding, so ff[b] counts exactly the bytes wholly inside.
-    const uint32_t nwr = (Lb + 31) >> 5;  // words of R
-    auto rword = [&](int64_t m) -> uint32_t {  // big-endian value of R word m (0 outside)
-        return (m >= 0 && m < (int64_t)nwr) ? __builtin_bswap32(R32[m]) : 0u;
-    };
+    // s = 8j - b.  Every run start was marked (y) and counted by s = -b (mod 8) as
+    // the words were stored; the last complete word and the final partial word are
+    // counted here, against zero padding.  Starts s < 0 (the byte split with the
+    // predecessor) do not exist and runs past Lb meet the zero padding, so ff[b]
+    // counts exactly the bytes wholly inside.
+    if (tid == 0) {
+        const uint32_t tail = (Lb & 31) ? L.carry : 0u;
+        if (has_pend) count_word(pend, tail);
+        if (Lb & 31) count_word(tail, 0u);
+    }
     {
-        uint32_t c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t m = tid; m < nwr; m += kK3Threads) {
-            const uint32_t x = rword(m), nx = rword((int64_t)m + 1);
-            uint32_t y = x;  // bit 31-t: stream bits [32m+t, 32m+t+8) are all ones
-#pragma unroll
-            for (int k = 1; k < 8; ++k) y &= __builtin_amdgcn_alignbit(x, nx, 32 - k);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) c8[(8 - r) & 7] += __builtin_popcount(y & (0x80808080u >> r));
-        }
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
             uint32_t s = c8[b];
