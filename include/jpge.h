@@ -93,7 +93,17 @@ int jpge_get_lanes(jpge_ctx* ctx, int* lanes);
  * 1..65535, else JPGE_E_ARG; the stripe phases (jpge_stripe_*) need mcus = 0. */
 int jpge_set_restart_interval(jpge_ctx* ctx, uint32_t mcus);
 
-/* Worst-case .jpg size for a frame (header + 2x worst-case entropy + RST markers + EOI). */
+/* Chroma subsampling for the context's following encodes: 420 (the default:
+ * applySubsampling(S420_m) as writeJPEG hard-codes it, Image.cpp:842, bit-identical
+ * to the reference) or 444 (applySubsampling(S444), Image.cpp:257-261: no
+ * subsampling; 8x8 MCUs of Y, Cb, Cr, all 1x1 in SOF0).  The reference's writeJPEG
+ * cannot emit 4:4:4; the oracle's S444 variant pins the bytes.  Other modes:
+ * JPGE_E_ARG.  jpge_fdct_quant then returns three full-resolution planes; the
+ * stripe phases (jpge_stripe_*) need 420. */
+int jpge_set_subsampling(jpge_ctx* ctx, int mode);
+
+/* Worst-case .jpg size for a frame, in either subsampling mode (header + 2x
+ * worst-case entropy + RST markers + EOI). */
 size_t jpge_max_jpeg_bytes(uint32_t width, uint32_t height);
 
 /* Quantisation tables for quality 1..100: the reference's Annex-K tables
@@ -116,7 +126,8 @@ int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy
 /* Stage entry — convertToColorSpace + applySubsampling(S420_m) + applyDCT(Arai) +
  * applyQuantization (Image.cpp:839-871) on the GPU: quantised coefficients before
  * DC differencing, per component, blocks in raster order, 64 natural-order values
- * per block (host buffers of (W'/8)(H'/8)*64 and 2 x (W'/16)(H'/16)*64 int16). */
+ * per block (host buffers of (W'/8)(H'/8)*64 and 2 x (W'/16)(H'/16)*64 int16; at
+ * 4:4:4 three buffers of ceil(W/8)*ceil(H/8)*64 int16). */
 int jpge_fdct_quant(jpge_ctx* ctx, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
                     int maxval, const uint8_t qy[64], const uint8_t qc[64], int16_t* coef_y, int16_t* coef_cb,
                     int16_t* coef_cr, uint32_t flags);

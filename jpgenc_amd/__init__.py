@@ -31,7 +31,8 @@ STATUS = {
 # every symbol include/jpge.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_open_ex", "jpge_close", "jpge_set_timing",
-    "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_set_restart_interval", "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
+    "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_set_restart_interval", "jpge_set_subsampling",
+    "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_encode_files", "jpge_synth_rgb8", "jpge_arai_constants",
     "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
@@ -99,6 +100,7 @@ def lib() -> ctypes.CDLL:
         L.jpge_reset_timing.argtypes = [vp]
         L.jpge_get_lanes.argtypes = [vp, ctypes.POINTER(i32)]
         L.jpge_set_restart_interval.argtypes = [vp, u32]
+        L.jpge_set_subsampling.argtypes = [vp, i32]
         L.jpge_device_count.argtypes = [ctypes.POINTER(i32)]
         L.jpge_max_jpeg_bytes.restype = sz
         L.jpge_max_jpeg_bytes.argtypes = [u32, u32]
@@ -279,6 +281,12 @@ class Encoder:
         """Restart interval in MCUs for the following encodes (0 = none: the reference's stream)."""
         _check(lib().jpge_set_restart_interval(self._ctx, int(mcus)), "set_restart_interval")
 
+    def set_subsampling(self, mode: int) -> None:
+        """Chroma subsampling for the following encodes: 420 (the reference's S420_m, the
+        default) or 444 (S444: no subsampling, 8x8 MCUs)."""
+        _check(lib().jpge_set_subsampling(self._ctx, int(mode)), "set_subsampling")
+        self._sub = int(mode)
+
     def lanes(self) -> int:
         n = ctypes.c_int32()
         _check(lib().jpge_get_lanes(self._ctx, ctypes.byref(n)), "get_lanes")
@@ -339,9 +347,13 @@ class Encoder:
         (nblocks, 64), blocks in raster order, natural order within a block."""
         rgb = np.ascontiguousarray(rgb, np.uint8)
         h, w = rgb.shape[:2]
-        W, H = (w + 15) // 16 * 16, (h + 15) // 16 * 16
-        y = np.zeros(((W // 8) * (H // 8), 64), np.int16)
-        cb = np.zeros(((W // 16) * (H // 16), 64), np.int16)
+        if getattr(self, "_sub", 420) == 444:
+            y = np.zeros((((w + 7) // 8) * ((h + 7) // 8), 64), np.int16)
+            cb = np.zeros_like(y)
+        else:
+            W, H = (w + 15) // 16 * 16, (h + 15) // 16 * 16
+            y = np.zeros(((W // 8) * (H // 8), 64), np.int16)
+            cb = np.zeros(((W // 16) * (H // 16), 64), np.int16)
         cr = np.zeros_like(cb)
         qy, qc = self._tables(quality, qy, qc)
         _check(lib().jpge_fdct_quant(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(y), _p(cb),

@@ -113,6 +113,11 @@ int jpge_set_restart_interval(jpge_ctx* ctx, uint32_t mcus) {
     return ctx->enc->set_restart(mcus) ? JPGE_E_ARG : JPGE_OK;
 }
 
+int jpge_set_subsampling(jpge_ctx* ctx, int mode) {
+    if (!ctx) return JPGE_E_ARG;
+    return ctx->enc->set_subsampling(mode) ? JPGE_E_ARG : JPGE_OK;
+}
+
 size_t jpge_max_jpeg_bytes(uint32_t w, uint32_t h) { return jpge::Encoder::max_jpeg_bytes(w, h); }
 
 int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]) {

@@ -72,8 +72,10 @@ constexpr int kPartsPerBlock = 4;  // lanes cooperating on one block's non-zero 
 
 // DC predecessor of flat block g (Image.cpp:638-678): the Y chain runs in MCU
 // order, Cb and Cr each over their own blocks; a chain's first block predicts 0.
-// The predecessor is at most 6 blocks back.
-__device__ __forceinline__ int64_t dc_pred_index(uint64_t g) {
+// The predecessor is at most 6 blocks back.  At 4:4:4 (bpm 3) every chain runs in
+// MCU order: the predecessor is the same slot of the previous MCU.
+__device__ __forceinline__ int64_t dc_pred_index(uint64_t g, uint32_t bpm) {
+    if (bpm == 3) return g < 3 ? -1 : (int64_t)g - 3;
     const int k = (int)(g % 6);
     if (k >= 1 && k <= 3) return (int64_t)g - 1;
     if (g < 6) return -1;
@@ -108,7 +110,7 @@ struct TileRegs {
             const int q = tid + i * kThreads;
             v[i] = q < nb * 8 ? src[q] : make_uint4(0, 0, 0, 0);
         }
-        prev_dc = (tid < 6 && b0 >= 6) ? coef[(b0 - 6 + tid) * 64] : 0;
+        prev_dc = (tid < 6 && b0 + tid >= 6) ? coef[(b0 - 6 + tid) * 64] : 0;
     }
 
     // zig-zag-ordered LDS blocks, the AC non-zero mask of every block (bit p =
@@ -144,17 +146,14 @@ struct TileRegs {
 // DC of the chain predecessor of block b0+blk (0 for a chain's first block and at a
 // restart interval's start), from the staged tile or the 6 DCs staged before it.
 __device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, const int* prevdc,
-                                       const DcSeed& seed, const Restart& rs) {
-    if (rs.mcus) {  // a restart interval's first MCU: Y00, Cb and Cr predict 0 again
-        const uint64_t g = b0 + blk;
-        const int k = (int)(g % 6);
-        if ((k == 0 || k >= 4) && (g / 6 + rs.mcu0) % rs.mcus == 0) return 0;
+                                       const DcSeed& seed, const Restart& rs, uint32_t bpm) {
+    const uint64_t g = b0 + blk;
+    const int k = (int)(g % bpm);
+    if (rs.mcus) {  // a restart interval's first MCU: its first Y, Cb and Cr predict 0 again
+        if ((k == 0 || k >= (int)bpm - 2) && (g / bpm + rs.mcu0) % rs.mcus == 0) return 0;
     }
-    const int64_t pg = dc_pred_index(b0 + blk);
-    if (pg < 0) {  // first MCU: the chain starts at 0, or at the previous stripe's last DC
-        const int k = (int)((b0 + blk) % 6);
-        return seed.v[k == 0 ? 0 : k - 3];
-    }
+    const int64_t pg = dc_pred_index(g, bpm);
+    if (pg < 0) return seed.v[block_comp(k, bpm)];  // first MCU: 0, or the previous stripe's last DC
     if (pg >= (int64_t)b0) return zz[(pg - (int64_t)b0) * kZzStride];
     return prevdc[pg - ((int64_t)b0 - 6)];
 }

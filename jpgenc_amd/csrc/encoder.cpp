@@ -27,12 +27,17 @@ namespace jpge {
 
 namespace {
 
-inline Geometry geometry(uint32_t w, uint32_t h) {
+// bpm 6: 4:2:0, 16x16 px MCUs; bpm 3: 4:4:4, 8x8 px MCUs (the frame cropped to whole
+// 8x8 blocks of the reference's 16-padded planes: the padding is edge replication
+// either way)
+inline Geometry geometry(uint32_t w, uint32_t h, uint32_t bpm = 6) {
     Geometry g;
     g.width = w;
     g.height = h;
-    g.mw = (w + 15) / 16;
-    g.mh = (h + 15) / 16;
+    g.bpm = bpm;
+    const uint32_t e = g.mcu_px();
+    g.mw = (w + e - 1) / e;
+    g.mh = (h + e - 1) / e;
     return g;
 }
 
@@ -191,7 +196,7 @@ struct Encoder::Slot {
     hipEvent_t ev[8] = {};
     Geometry g;
     // device workspace (capacities)
-    size_t cap_mcu = 0, cap_in = 0, cap_out = 0, cap_ctl = 0;
+    size_t cap_blk = 0, cap_in = 0, cap_out = 0, cap_ctl = 0;
     uint8_t* d_in = nullptr;
     int16_t* d_coef = nullptr;
     uint8_t* d_ctl = nullptr;
@@ -300,12 +305,23 @@ int Encoder::set_restart(uint32_t mcus) {
     return kOk;
 }
 
+int Encoder::set_subsampling(int mode) {
+    if (mode != 420 && mode != 444) return kErrArg;
+    bpm_ = mode == 444 ? 3u : 6u;
+    return kOk;
+}
+
 size_t Encoder::max_jpeg_bytes(uint32_t w, uint32_t h) {
     // header <= 20 + 2*69 + 19 + 4*(4+17+256) + 14 ; entropy <= 1665 bits/block,
     // doubled for worst-case 0xFF stuffing; + EOI.
     // Restart intervals add per MCU at most an RST marker, a fill byte and its stuffing.
-    const Geometry g = geometry(w, h);
-    return 2048 + (size_t)g.nblocks() * 2 * 209 + 16 + (size_t)g.nmcu() * 4;
+    // (The larger of the 4:2:0 and 4:4:4 bounds: one capacity serves either mode.)
+    size_t cap = 0;
+    for (uint32_t bpm : {6u, 3u}) {
+        const Geometry g = geometry(w, h, bpm);
+        cap = std::max(cap, 2048 + (size_t)g.nblocks() * 2 * 209 + 16 + (size_t)g.nmcu() * 4);
+    }
+    return cap;
 }
 
 int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
@@ -396,12 +412,12 @@ void Encoder::dump_stamps(const Slot& s) {
 }
 
 int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap) {
-    const size_t nmcu = g.nmcu();
-    if (nmcu > s.cap_mcu) {
+    const size_t nblk = g.nblocks();
+    if (nblk > s.cap_blk) {
         hipFree(s.d_coef);
-        s.d_coef = nullptr; s.cap_mcu = 0;
-        JPGE_HIP(hipMalloc((void**)&s.d_coef, nmcu * 768));
-        s.cap_mcu = nmcu;
+        s.d_coef = nullptr; s.cap_blk = 0;
+        JPGE_HIP(hipMalloc((void**)&s.d_coef, nblk * 128));
+        s.cap_blk = nblk;
     }
     const CtlLayout L(layout(g).grid());
     const size_t ubuf = entropy_ubuf_bytes(layout(g));
@@ -506,7 +522,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
                     Slot* imp, bool export_hist) {
     if (!f.rgb || f.width == 0 || f.height == 0 || f.width > 65535 || f.height > 65535) return kErrArg;
     if (f.maxval < 1 || f.maxval > 255) return kErrRange;
-    const Geometry g = geometry(f.width, f.height);
+    const Geometry g = geometry(f.width, f.height, bpm_);
     const size_t row = (size_t)f.width * 3;
     const size_t stride = f.stride ? f.stride : row;
     if (stride < row) return kErrArg;
@@ -594,7 +610,7 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
     if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
-    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_);
+    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_, s.g.s444());
     if (hdr.size() > kHdrMax) return kErrInternal;
     std::memcpy(reinterpret_cast<uint8_t*>(s.h_tab) + kTabBytes, hdr.data(), hdr.size());
     s.hdr_len = hdr.size();
@@ -855,16 +871,18 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
     if (st) { hipStreamSynchronize(s.stream); return st; }
     JPGE_HIP(hipStreamSynchronize(s.stream));
     const Geometry& g = s.g;
-    std::vector<int16_t> coef((size_t)g.nmcu() * 384);
+    std::vector<int16_t> coef((size_t)g.nblocks() * 64);
     JPGE_HIP(hipMemcpy(coef.data(), s.d_coef, coef.size() * 2, hipMemcpyDeviceToHost));
-    const uint32_t ybw = 2 * g.mw, cbw = g.mw;
+    const uint32_t ybw = (g.bpm == 3 ? 1 : 2) * g.mw, cbw = g.mw;
     for (uint32_t m = 0; m < g.nmcu(); ++m) {
         const uint32_t mr = m / g.mw, mc = m % g.mw;
-        for (int k = 0; k < 6; ++k) {
-            const int16_t* src = &coef[((size_t)m * 6 + k) * 64];
+        for (int k = 0; k < (int)g.bpm; ++k) {
+            const int16_t* src = &coef[((size_t)m * g.bpm + k) * 64];
+            const int comp = block_comp(k, g.bpm);
             int16_t* dst;
-            if (k < 4) dst = y + ((size_t)(2 * mr + (k >> 1)) * ybw + 2 * mc + (k & 1)) * 64;
-            else dst = (k == 4 ? cb : cr) + ((size_t)mr * cbw + mc) * 64;
+            if (comp == 0 && g.bpm == 3) dst = y + (size_t)m * 64;
+            else if (comp == 0) dst = y + ((size_t)(2 * mr + (k >> 1)) * ybw + 2 * mc + (k & 1)) * 64;
+            else dst = (comp == 1 ? cb : cr) + ((size_t)mr * cbw + mc) * 64;
             for (int i = 0; i < 64; ++i) dst[i] = src[i];
         }
     }
@@ -896,6 +914,7 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
 int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]) {
     JPGE_HIP(hipSetDevice(device_));
     if (!d.rgb || !last_dc || d.width == 0 || d.height == 0 || d.width > 65535 || d.height > 65535) return kErrArg;
+    if (bpm_ != 6) return kErrArg;  // stripes are 4:2:0 (the reference's subsampling)
     if (d.maxval < 1 || d.maxval > 255) return kErrRange;
     const uint32_t mh_img = (d.height + 15) / 16;
     if (d.mcu_rows == 0 || d.mcu_row0 >= mh_img || d.mcu_rows > mh_img - d.mcu_row0) return kErrArg;

@@ -112,17 +112,18 @@ struct PartCoder {
 };
 
 __device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int nb, int blk, int part,
-                                                const DcSeed& seed, const Restart& rs) {
+                                                const DcSeed& seed, const Restart& rs, uint32_t bpm) {
     PartCoder c;
     c.part = part;
     c.active = blk < nb;
-    const int k = (int)((b0 + blk) % 6);
-    c.tdc = &L.tab[(k < 4 ? 0 : 2) * 256];
-    c.tac = &L.tab[(k < 4 ? 1 : 3) * 256];
+    const bool chroma = block_comp((int)((b0 + blk) % bpm), bpm) != 0;
+    c.tdc = &L.tab[(chroma ? 2 : 0) * 256];
+    c.tac = &L.tab[(chroma ? 3 : 1) * 256];
     c.mask = c.active ? L.bmask[blk] : 0ull;
     c.pv.load(L.u.zz, c.mask, blk, part, c.active);
     // DC difference to the chain predecessor, Image.cpp:638-678
-    c.dcdiff = (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc, seed, rs) : 0;
+    c.dcdiff =
+        (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc, seed, rs, bpm) : 0;
     return c;
 }
 
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         JPGE_ACC(0, tq);
         uint32_t n;  // bits of this lane's part
         {
-            const PartCoder pc = make_coder(L, b0, nb, blk, part, a.seed, a.rst);
+            const PartCoder pc = make_coder(L, b0, nb, blk, part, a.seed, a.rst, a.g.bpm);
             SlotSink ss;
             ss.init(L.slot + tid);
             n = code_part(pc, ss);
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
         wl += T;
         JPGE_ACC(4, tq);
     }
-    const uint32_t Lb = wl;  // this workgroup's bits (>= 12: every block codes >= 2 bits)
+    const uint32_t Lb = wl;  // this workgroup's bits (>= 6: every block codes >= 2 bits, >= 3 blocks)
     if (tid == 0 && (Lb & 31)) R32[Lb >> 5] = __builtin_bswap32(L.carry);
     vm_drain();
     __syncthreads();
@@ -283,10 +284,17 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     if (tid < 3) {
         uint32_t* rec = reinterpret_cast<uint32_t*>(a.rec + (uint64_t)wg * kEntropyRecordBytes);
         if (tid == 0) {
-            // first 8 bits; last 8 bits (the 16-bit window holding them is inside R)
+            // first 8 bits; last 8 bits (the 16-bit window holding them is inside R).
+            // A stream shorter than a byte (a 4:4:4 restart interval of one MCU) is
+            // only ever placed byte-aligned: its "last 8 bits" are its bits, right-aligned.
             const uint32_t head = R8[0];
-            const uint32_t s0 = Lb - 8, byte = s0 >> 3, sh = s0 & 7;
-            const uint32_t tail = ((((uint32_t)R8[byte] << 8) | R8[byte + 1]) >> (8 - sh)) & 0xFF;
+            uint32_t tail;
+            if (Lb >= 8) {
+                const uint32_t s0 = Lb - 8, byte = s0 >> 3, sh = s0 & 7;
+                tail = ((((uint32_t)R8[byte] << 8) | R8[byte + 1]) >> (8 - sh)) & 0xFF;
+            } else {
+                tail = (uint32_t)R8[0] >> (8 - Lb);
+            }
             *reinterpret_cast<uint4*>(rec + 8) = make_uint4(Lb, head | (tail << 8), 0u, 0u);
         } else {
             const int b0 = 4 * (tid - 1);  // ff[0..3], ff[4..7]
@@ -659,14 +667,14 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
 // all (two per CU: LDS, registers) unless overridden.  One segment (restart off):
 // 128-block tiles, at least two per workgroup when the frame has two (so a
 // workgroup's stream holds >= 8 bits: its first and last 8 bits, which the
-// placement reads, are defined).  Restart intervals of R MCUs: segments of 6R
-// blocks (>= 6 blocks, >= 12 bits), each cut into balanced tiles of <= 128 blocks,
-// a whole number of workgroups per segment.
+// placement reads, are defined).  Restart intervals of R MCUs: segments of bpm*R
+// blocks (>= 3 blocks, >= 6 bits; each starts byte-aligned), each cut into
+// balanced tiles of <= 128 blocks, a whole number of workgroups per segment.
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override) {
     SegLayout L;
     const uint32_t nb = g.nblocks();
     const uint32_t want = wgs_override ? wgs_override : 512u;
-    const uint64_t S = 6ull * restart_mcus;
+    const uint64_t S = (uint64_t)g.bpm * restart_mcus;
     if (!restart_mcus || S >= nb) {
         const uint32_t nt = (nb + kK3Blocks - 1) / kK3Blocks;
         uint32_t G = 1;

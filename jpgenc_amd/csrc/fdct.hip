@@ -364,10 +364,196 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     JPGE_STAMP(7);
 }
 
+// ---- 4:4:4 (S444 extension: applySubsampling(S444), Image.cpp:257-261, is the
+// identity; MCU = one 8x8 block of each of Y, Cb, Cr) ----
+// Same machinery as fdct_kernel: a wave owns a tile of 16 MCUs (128x8 px; a lane
+// stages one 16-px run of one row), in six rounds of 8 blocks: Y MCUs 0-7, Y MCUs
+// 8-15, Cb 0-7, Cb 8-15, Cr 0-7, Cr 8-15 (lane = (block of the round, column)).
+// Chroma is converted per pixel: for 8-bit input (128 + v) - 128 == v exactly, and
+// v = fma(kb, b, fma(kg, g, kr r)) is exact.
+constexpr int kRgbPitch444 = 130;  // u32 per staged row of 128 px (+2: even, for uint2 stores)
+static_assert(8 * kRgbPitch444 <= 16 * kRgbPitch, "the 4:4:4 tile fits the 4:2:0 staging area");
+
+__device__ __forceinline__ double ycc_exact_c(uint32_t p, double kr, double kg, double kb) {
+    const double r = (double)(p & 0xFF), g = (double)((p >> 8) & 0xFF), b = (double)(p >> 16);
+    return __builtin_fma(kb, b, __builtin_fma(kg, g, kr * r));
+}
+
+template <bool kExact, int kWaves>
+__global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
+    constexpr int kK1Threads = kWaves * 64;
+    __shared__ K1Lds<kWaves> lds;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    K1WaveLds& W = lds.w[wv];
+    JPGE_STAMP(1);
+    const uint32_t mw = a.g.mw;
+    const uint32_t tiles_per_row = (mw + 15) / 16;
+    const uint32_t ntiles = tiles_per_row * a.g.mh;
+    const double scale = 255.0 / (double)a.maxval;  // Image.cpp:465
+    const bool aligned = (((uintptr_t)a.rgb | a.stride) & 15) == 0;
+    const int r8 = lane >> 3, c8 = lane & 7;  // staging: lane -> (pixel row, 16-px chunk)
+    const int b8 = lane >> 3, j = lane & 7;   // DCT: lane -> (block of the round, column)
+
+    const __amdgpu_buffer_rsrc_t rgb_rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(a.rgb), 0, (int)(uint32_t)((uint64_t)a.stride * (a.g.height - 1) + 3ull * a.g.width),
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t coef_rs =
+        __builtin_amdgcn_make_buffer_rsrc(a.coef, 0, (int)(uint32_t)((uint64_t)a.g.nblocks() * 128), 0x00020000);
+
+    // dynamic tiles over the workgroup's contiguous run, as in fdct_kernel
+    const uint32_t tb_p = (uint32_t)((uint64_t)ntiles * blockIdx.x / gridDim.x);
+    const uint32_t n_p = (uint32_t)((uint64_t)ntiles * (blockIdx.x + 1) / gridDim.x) - tb_p;
+    auto grab = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(&lds.next, 1u);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
+        const uint32_t t = tb_p + k;
+        const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * 16;
+        const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 + c8 * 16;
+        const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
+        const uint32_t off = ok ? (uint32_t)((uint64_t)y * a.stride + (uint64_t)xs * 3) : kOob;
+        v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
+        v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
+        v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, K1_LOAD_AUX));
+        return ok;
+    };
+    u32x4 pend;
+    uint32_t poff = kOob;
+    auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, K1_STORE_AUX); };
+    uint32_t k = wv;
+    uint4 c0, c1, c2;
+    bool cfast = fast_load(k, c0, c1, c2);
+
+    for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
+    if (blockIdx.x == 0)
+        for (uint32_t i = tid; i < a.imp_n16; i += kK1Threads) a.imp_dst[i] = a.imp_src[i];
+    if (tid == 0) lds.next = kWaves;
+    if (tid < 128) {
+        const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
+        const double q = (double)a.q[tid];
+        lds.q[c][o] = q;
+        lds.invq[c][o] = kS[e & 7] / q;
+    }
+    __syncthreads();
+    JPGE_STAMP(0);
+    uint32_t kn = k < n_p ? grab() : n_p;
+
+    double* tb = &W.tmp[b8 * kTmpBlock];
+    auto load_px = [&](int round, uint32_t p[8]) {  // column j of the round's block b8
+        const int col = ((round & 1) * 8 + b8) * 8 + j;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[i] = W.rgbx[i * kRgbPitch444 + col];
+    };
+    auto load_iq = [&](int qb, double iq[8]) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) iq[u] = lds.invq[qb][j * kQRow + u];
+    };
+
+    for (; k < n_p;) {
+        const uint32_t t = tb_p + k;
+        const uint32_t mrow = t / tiles_per_row;
+        const uint32_t mcol0 = (t % tiles_per_row) * 16;
+        const int nvalid = (int)min(16u, mw - mcol0);
+        const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 + c8 * 16;
+
+        uint32_t px[16];
+        {
+            const uint4 v0 = c0, v1 = c1, v2 = c2;
+            const uint32_t wd[13] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, 0u};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int b0 = 3 * i, d = b0 >> 2;
+                const uint32_t o8 = (uint32_t)(b0 & 3);
+                px[i] = __builtin_amdgcn_perm(wd[d + 1], wd[d], 0x0C000000u | ((o8 + 2) << 16) | ((o8 + 1) << 8) | o8);
+            }
+        }
+        if (!cfast) {  // edge replication (Image.cpp:498-531) as clamped addressing
+            const uint32_t sy = min(y, a.g.height - 1);
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t sx = min(xs + i, a.g.width - 1);
+                const uint8_t* p = a.rgb + (uint64_t)sy * a.stride + (uint64_t)sx * 3;
+                px[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+            }
+        }
+        uint32_t* dst = &W.rgbx[r8 * kRgbPitch444 + c8 * 16];
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) *reinterpret_cast<uint2*>(dst + i) = make_uint2(px[i], px[i + 1]);
+        wave_order();
+        store_pending();
+        cfast = fast_load(kn, c0, c1, c2);
+        const uint32_t kn2 = kn < n_p ? grab() : n_p;
+
+        uint32_t p[8];
+        double iq[8];
+        load_px(0, p);
+        load_iq(0, iq);
+        wave_order();
+#pragma unroll
+        for (int round = 0; round < 6; ++round) {
+            const int comp = round >> 1, m = (round & 1) * 8 + b8, qb = comp ? 1 : 0;
+            double x[8];
+            if (comp == 0) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) x[i] = kExact ? ycc_exact_y(p[i]) : ycc_ref_y(p[i], scale);
+            } else {
+                const double kr = comp == 2 ? kCrR : kCbR, kg = comp == 2 ? kCrG : kCbG, kb = comp == 2 ? kCrB : kCbB;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    x[i] = kExact ? ycc_exact_c(p[i], kr, kg, kb) : ycc_ref_c(p[i], scale, kr, kg, kb);
+            }
+            double o[8];
+            arai8(x, o);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) tb[j * kTmpRow + u] = o[u];
+            wave_order();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = tb[i * kTmpRow + j];
+            double iqc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) iqc[u] = iq[u];
+            wave_order();
+            if (round + 1 < 6) {  // the next round's inputs, after this round's LDS reads
+                load_px(round + 1, p);
+                if (round == 1) load_iq(1, iq);
+            }
+            arai8_unscaled(x, o);
+            int qv[8];
+            bool near_half = false;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) qv[u] = quant_fast(o[u], iqc[u], near_half);
+            if (__builtin_amdgcn_ballot_w64(near_half)) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], kS[u], lds.q[qb][j * kQRow + u]);
+            }
+            const uint32_t blk = (mrow * mw + mcol0 + m) * 3 + comp;
+            const uint32_t off = m < nvalid ? blk * 128 + j * 16 : kOob;
+            u32x4 pk;
+            pk.x = __builtin_amdgcn_perm((uint32_t)qv[1], (uint32_t)qv[0], 0x05040100u);
+            pk.y = __builtin_amdgcn_perm((uint32_t)qv[3], (uint32_t)qv[2], 0x05040100u);
+            pk.z = __builtin_amdgcn_perm((uint32_t)qv[5], (uint32_t)qv[4], 0x05040100u);
+            pk.w = __builtin_amdgcn_perm((uint32_t)qv[7], (uint32_t)qv[6], 0x05040100u);
+            if (round < 5) {
+                __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
+            } else {
+                pend = pk;
+                poff = off;
+            }
+        }
+        wave_order();  // the next tile's staging overwrites the transpose buffer
+        k = kn;
+        kn = kn2;
+    }
+    store_pending();
+    __syncthreads();
+    JPGE_STAMP(7);
+}
+
 }  // namespace
 
 uint32_t fdct_grid(const Geometry& g, bool solo) {
-    const uint32_t tiles = ((g.mw + 3) / 4) * g.mh;
+    const uint32_t tiles = ((g.mw + (g.s444() ? 15 : 3)) / (g.s444() ? 16 : 4)) * g.mh;
     // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
     const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
     const uint32_t cap = solo ? 256u : 1024u;
@@ -379,6 +565,17 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
     // (a 16384^2 frame needs 805 MB of each)
     if ((uint64_t)a.stride * a.g.height >= kOob || (uint64_t)a.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
     const uint32_t grid = fdct_grid(a.g, a.solo);
+    if (a.g.s444()) {
+        const bool ex = a.maxval == 255;
+        if (a.solo) {
+            if (ex) hipLaunchKernelGGL((fdct444_kernel<true, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+            else hipLaunchKernelGGL((fdct444_kernel<false, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+        } else {
+            if (ex) hipLaunchKernelGGL((fdct444_kernel<true, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+            else hipLaunchKernelGGL((fdct444_kernel<false, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        }
+        return hipGetLastError();
+    }
     if (a.solo) {
         if (a.maxval == 255)
             hipLaunchKernelGGL((fdct_kernel<true, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);

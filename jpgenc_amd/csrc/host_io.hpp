@@ -54,9 +54,10 @@ extern const uint8_t kZigzagToNatural[64];
 
 // SOI, APP0, DQT(luma), DQT(chroma), SOF0, DHT x4, SOS, in that order
 // (Image.cpp:936-954).  tables: Y-DC, Y-AC, C-DC, C-AC.  restart_mcus > 0 adds a DRI
-// segment before SOS (not in the reference).
+// segment before SOS, s444 declares Y 1x1 (both not in the reference).
 std::vector<uint8_t> jfif_headers(uint32_t real_width, uint32_t real_height, const uint8_t qy[64],
-                                  const uint8_t qc[64], const HuffTable* const tables[4], uint32_t restart_mcus = 0);
+                                  const uint8_t qc[64], const HuffTable* const tables[4], uint32_t restart_mcus = 0,
+                                  bool s444 = false);
 
 // Deterministic synthetic RGB8 frame (integer-only, identical on every host):
 // kind 0 = smooth gradients + texture + noise (photo-like), 1 = uniform random

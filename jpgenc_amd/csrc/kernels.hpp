@@ -24,12 +24,19 @@ namespace jpge {
 
 // Frame geometry (reference: Image.cpp:480-531 pads to 16, Image.cpp:311-312
 // halves the chroma planes).  One MCU = 16x16 px = Y00 Y01 Y10 Y11 Cb Cr.
+// bpm = blocks per MCU: 6 at 4:2:0 (the reference's S420_m: 16x16 px MCUs of
+// Y00 Y01 Y10 Y11 Cb Cr), 3 at 4:4:4 (the S444 extension: 8x8 px MCUs of Y Cb Cr).
 struct Geometry {
     uint32_t width = 0, height = 0;  // real size
     uint32_t mw = 0, mh = 0;         // MCUs per row / column
+    uint32_t bpm = 6;
     JPGE_HD uint32_t nmcu() const { return mw * mh; }
-    JPGE_HD uint32_t nblocks() const { return nmcu() * 6; }
+    JPGE_HD uint32_t nblocks() const { return nmcu() * bpm; }
+    JPGE_HD bool s444() const { return bpm == 3; }
+    JPGE_HD uint32_t mcu_px() const { return bpm == 3 ? 8u : 16u; }  // MCU edge in pixels
 };
+// component of MCU slot k: 0 = Y, 1 = Cb, 2 = Cr (the last two slots are the chroma)
+JPGE_HD inline int block_comp(int k, uint32_t bpm) { return k < (int)bpm - 2 ? 0 : k - ((int)bpm - 3); }
 
 constexpr int kHistReplicas = 8;          // spread of the global histogram atomics
 constexpr int kStatsTile = 128;           // blocks per statistics tile (4 lanes each)

@@ -43,8 +43,9 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     JPGE_STAMP(0);
     // key bases: Y raster index of the first Y block row of this workgroup's first
     // MCU row, chroma raster index of that MCU row (keys are relative to them)
-    const uint32_t mrow0 = (uint32_t)(((uint64_t)t_first * kK2Blocks) / 6) / mw;
-    const uint64_t ybase = 2ull * mrow0 * (2ull * mw);
+    const uint32_t bpm = a.g.bpm;  // 6 (4:2:0) or 3 (4:4:4: the Y text is in MCU order)
+    const uint32_t mrow0 = (uint32_t)(((uint64_t)t_first * kK2Blocks) / bpm) / mw;
+    const uint64_t ybase = bpm == 3 ? (uint64_t)mrow0 * mw : 2ull * mrow0 * (2ull * mw);
     const uint64_t cbase = (uint64_t)mrow0 * mw;
     const int lane = tid & 63, wv = tid >> 6;
     const int blk = block_of(wv, lane), part = part_of(wv);
@@ -65,23 +66,28 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         JPGE_ACC(0, tq);
         const bool active = blk < nb;
         const uint64_t g = b0 + blk;
-        const int k = (int)(g % 6);
-        const uint64_t m6 = g / 6;
-        const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
+        const int k = (int)(g % bpm);
+        const uint64_t m6 = g / bpm;
+        const int comp = block_comp(k, bpm);
         uint32_t rel;  // index of this block in its symbol text, relative to the bases
         int tsel;
-        if (k < 4) {
-            rel = (uint32_t)((2ull * mrow + (k >> 1)) * (2ull * mw) + 2ull * mcol + (k & 1) - ybase);
+        if (comp == 0) {
+            if (bpm == 3) {
+                rel = (uint32_t)(m6 - ybase);
+            } else {
+                const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
+                rel = (uint32_t)((2ull * mrow + (k >> 1)) * (2ull * mw) + 2ull * mcol + (k & 1) - ybase);
+            }
             tsel = 0;
         } else {
-            rel = (uint32_t)(m6 - cbase) | (k == 5 ? 0x80000000u : 0u);  // all Cr after all Cb
+            rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);  // all Cr after all Cb
             tsel = 1;
         }
         const uint64_t mask = lds.bmask[blk];
         PartView pv;
         pv.load(lds.zz, mask, blk, part, active);
         if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
-            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst));
+            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst, bpm));
             atomicAdd(&lds.dcnt[tsel][dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);

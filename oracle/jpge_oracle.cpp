@@ -403,6 +403,49 @@ void dc_diff_restart(Frame& f, int R) {
         }
 }
 
+// S444 variant (not in the reference's writeJPEG, which hard-codes S420_m at
+// Image.cpp:842): applySubsampling(S444) (Image.cpp:257-261) leaves Cb and Cr at full
+// resolution, and the MCU is one 8x8 block of each component.  The planes are cropped
+// to whole blocks, ceil(w/8)*8 x ceil(h/8)*8, of the reference's 16-padded planes
+// (edge replication either way: a decoder expects ceil(w/8) x ceil(h/8) MCUs).
+void run_to_quant444(Frame& f, const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy,
+                     const uint8_t* qc) {
+    load_planes(f, rgb, w, h, maxval);
+    to_ycc(f);
+    f.R.clear(); f.G.clear(); f.B.clear();
+    const int W8 = (w + 7) / 8 * 8, H8 = (h + 7) / 8 * 8;
+    for (std::vector<double>* p : {&f.Y, &f.Cb, &f.Cr}) {
+        std::vector<double> o((size_t)W8 * H8);
+        for (int y = 0; y < H8; ++y)
+            for (int x = 0; x < W8; ++x) o[(size_t)y * W8 + x] = (*p)[(size_t)y * f.W + x];
+        p->swap(o);
+    }
+    f.W = f.sw = W8;
+    f.H = f.sh = H8;
+    dct_plane(f.Y, W8, H8, f.dY);
+    dct_plane(f.Cb, W8, H8, f.dCb);
+    dct_plane(f.Cr, W8, H8, f.dCr);
+    quant_plane(f.dY, W8, H8, qy, f.qY);
+    quant_plane(f.dCb, W8, H8, qc, f.qCb);
+    quant_plane(f.dCr, W8, H8, qc, f.qCr);
+}
+
+// DC chains at 4:4:4 (Image.cpp:638-678 applied per component): each component's
+// blocks in raster order, which is MCU order; restart R > 0 resets all three at the
+// first MCU of every interval.
+void dc_diff444(Frame& f, int R) {
+    int b[3] = {0, 0, 0}, m = 0;
+    std::vector<int>* pl[3] = {&f.qY, &f.qCb, &f.qCr};
+    for (int h = 0; h < f.H; h += 8)
+        for (int w = 0; w < f.W; w += 8, ++m) {
+            if (R && m % R == 0) b[0] = b[1] = b[2] = 0;
+            for (int c = 0; c < 3; ++c) {
+                int& v = (*pl[c])[(size_t)h * f.W + w];
+                int t = v; v = t - b[c]; b[c] = t;
+            }
+        }
+}
+
 void block_syms(const std::vector<int>& plane, int W, int H, std::vector<std::vector<Sym>>& out) {
     int bw = W / 8, bh = H / 8;
     out.assign((size_t)bw * bh, {});
@@ -419,7 +462,7 @@ void put_u16(std::vector<uint8_t>& o, int v) { o.push_back((uint8_t)(v >> 8)); o
 
 // JFIF segments, JpegSegments.hpp:55-377 as used by Image.cpp:933-972.
 void write_headers(std::vector<uint8_t>& o, int rw, int rh, const uint8_t qy[64], const uint8_t qc[64],
-                   const Table* t[4], int restart = 0) {
+                   const Table* t[4], int restart = 0, bool s444 = false) {
     const uint8_t soi_app0[] = {0xFF, 0xD8, 0xFF, 0xE0, 0, 16, 'J', 'F', 'I', 'F', 0, 1, 1, 0, 0, 1, 0, 1, 0, 0};
     o.insert(o.end(), soi_app0, soi_app0 + sizeof(soi_app0));
     const uint8_t* qt[2] = {qy, qc};
@@ -429,7 +472,7 @@ void write_headers(std::vector<uint8_t>& o, int rw, int rh, const uint8_t qy[64]
     }
     o.push_back(0xFF); o.push_back(0xC0); put_u16(o, 17); o.push_back(8);
     put_u16(o, rh & 0xFFFF); put_u16(o, rw & 0xFFFF); o.push_back(3);
-    const uint8_t comp[9] = {1, 0x22, 0, 2, 0x11, 1, 3, 0x11, 1};
+    const uint8_t comp[9] = {1, (uint8_t)(s444 ? 0x11 : 0x22), 0, 2, 0x11, 1, 3, 0x11, 1};
     o.insert(o.end(), comp, comp + 9);
     const uint8_t info[4] = {0x00, 0x10, 0x01, 0x11};
     for (int k = 0; k < 4; ++k) {
@@ -459,13 +502,19 @@ void emit_block(BitWriter& bw, const std::vector<Sym>& s, const Table& dc, const
 // restart = 0: writeJPEG (Image.cpp:831-1006).  restart = R > 0: the restart-interval
 // variant — DC chains reset per interval, and after every interval but the last the
 // stream is 1-filled, stuffed and followed by RSTn (n = interval index mod 8).
+// s444: the S444 variant (run_to_quant444; Y 1x1 in SOF0; MCU = Y, Cb, Cr).
 int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
-                 std::vector<uint8_t>& out, int restart = 0) {
+                 std::vector<uint8_t>& out, int restart = 0, bool s444 = false) {
     if (w <= 0 || h <= 0 || maxval <= 0 || maxval > 255 || restart < 0 || restart > 65535) return -1;
     Frame f;
-    run_to_quant(f, rgb, w, h, maxval, qy, qc);
-    if (restart) dc_diff_restart(f, restart);
-    else dc_diff(f);
+    if (s444) {
+        run_to_quant444(f, rgb, w, h, maxval, qy, qc);
+        dc_diff444(f, restart);
+    } else {
+        run_to_quant(f, rgb, w, h, maxval, qy, qc);
+        if (restart) dc_diff_restart(f, restart);
+        else dc_diff(f);
+    }
     std::vector<std::vector<Sym>> sY, sCb, sCr;
     block_syms(f.qY, f.W, f.H, sY);
     block_syms(f.qCb, f.sw, f.sh, sCb);
@@ -478,8 +527,8 @@ int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy
     Table tyd = build_table(ydc), tya = build_table(yac), tcd = build_table(cdc), tca = build_table(cac);
     const Table* tabs[4] = {&tyd, &tya, &tcd, &tca};
     out.clear();
-    write_headers(out, f.rw, f.rh, qy, qc, tabs, restart);
-    // MCU interleave, Image.cpp:957-968
+    write_headers(out, f.rw, f.rh, qy, qc, tabs, restart, s444);
+    // MCU interleave, Image.cpp:957-968 (at 4:4:4 one block of each component)
     BitWriter bw;
     int ybw = f.W / 8, cbw = f.sw / 8, cbh = f.sh / 8;
     int mcu = 0;
@@ -491,10 +540,14 @@ int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy
                 out.push_back(0xFF); out.push_back((uint8_t)(0xD0 + ((mcu / restart - 1) & 7)));
                 bw = BitWriter();
             }
-            emit_block(bw, sY[(size_t)(2 * i) * ybw + 2 * j], tyd, tya);
-            emit_block(bw, sY[(size_t)(2 * i) * ybw + 2 * j + 1], tyd, tya);
-            emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j], tyd, tya);
-            emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j + 1], tyd, tya);
+            if (s444) {
+                emit_block(bw, sY[(size_t)i * ybw + j], tyd, tya);
+            } else {
+                emit_block(bw, sY[(size_t)(2 * i) * ybw + 2 * j], tyd, tya);
+                emit_block(bw, sY[(size_t)(2 * i) * ybw + 2 * j + 1], tyd, tya);
+                emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j], tyd, tya);
+                emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j + 1], tyd, tya);
+            }
             emit_block(bw, sCb[(size_t)i * cbw + j], tcd, tca);
             emit_block(bw, sCr[(size_t)i * cbw + j], tcd, tca);
         }
@@ -709,6 +762,36 @@ int64_t orc_encode_rgb_restart(const uint8_t* rgb, int w, int h, int maxval, con
     if ((int64_t)o.size() > cap) return -(int64_t)o.size();
     memcpy(out, o.data(), o.size());
     return (int64_t)o.size();
+}
+
+// Either variant: restart MCUs per interval (0 = none), subsampling 420 or 444.
+int64_t orc_encode_rgb_ex(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                          int restart, int subsampling, uint8_t* out, int64_t cap) {
+    if (subsampling != 420 && subsampling != 444) return -1;
+    std::vector<uint8_t> o;
+    if (encode_frame(rgb, w, h, maxval, qy, qc, o, restart, subsampling == 444) != 0) return -1;
+    if ((int64_t)o.size() > cap) return -(int64_t)o.size();
+    memcpy(out, o.data(), o.size());
+    return (int64_t)o.size();
+}
+
+// Stage dump of the S444 variant: quantised coefficients before DC differencing,
+// three planes of ceil(w/8) x ceil(h/8) blocks in raster order.
+int orc_stage_coeffs444(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                        int16_t* outY, int16_t* outCb, int16_t* outCr) {
+    Frame f;
+    run_to_quant444(f, rgb, w, h, maxval, qy, qc);
+    const int bw = f.W / 8, bh = f.H / 8;
+    const std::vector<int>* pl[3] = {&f.qY, &f.qCb, &f.qCr};
+    int16_t* o[3] = {outY, outCb, outCr};
+    for (int c = 0; c < 3; ++c)
+        for (int by = 0; by < bh; ++by)
+            for (int bx = 0; bx < bw; ++bx)
+                for (int i = 0; i < 8; ++i)
+                    for (int j = 0; j < 8; ++j)
+                        o[c][((size_t)by * bw + bx) * 64 + i * 8 + j] =
+                            (int16_t)(*pl[c])[(size_t)(by * 8 + i) * f.W + bx * 8 + j];
+    return 0;
 }
 
 int orc_set_threads(int n) {

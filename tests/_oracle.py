@@ -48,6 +48,9 @@ def orc() -> ctypes.CDLL:
         L.orc_encode_rgb.argtypes = [vp, i32, i32, i32, vp, vp, vp, i64]
         L.orc_encode_rgb_restart.restype = i64
         L.orc_encode_rgb_restart.argtypes = [vp, i32, i32, i32, vp, vp, i32, vp, i64]
+        L.orc_encode_rgb_ex.restype = i64
+        L.orc_encode_rgb_ex.argtypes = [vp, i32, i32, i32, vp, vp, i32, i32, vp, i64]
+        L.orc_stage_coeffs444.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
         L.orc_set_threads.argtypes = [i32]
         _orc = L
     return _orc
@@ -85,16 +88,21 @@ def huffman(text, lib=None, fn="orc_huffman"):
     return list(zip(s[:k].tolist(), ln[:k].tolist(), c[:k].tolist()))
 
 
-def encode(rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None, restart: int = 0) -> bytes:
-    """writeJPEG; restart > 0: the restart-interval variant (DRI + RSTn every `restart` MCUs)."""
+def encode(rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None, restart: int = 0,
+           subsampling: int = 420) -> bytes:
+    """writeJPEG; restart > 0: the restart-interval variant (DRI + RSTn every `restart` MCUs);
+    subsampling 444: the S444 variant."""
     rgb = np.ascontiguousarray(rgb, np.uint8)
     h, w = rgb.shape[:2]
     if qy is None:
         qy, qc = quality_tables(quality)
-    cap = 4096 + ((w + 15) // 16) * ((h + 15) // 16) * (6 * 420 + 4)
+    cap = 4096 + ((w + 7) // 8) * ((h + 7) // 8) * (3 * 420 + 4)
     out = np.empty(cap, np.uint8)
     qy8, qc8 = np.ascontiguousarray(qy, np.uint8), np.ascontiguousarray(qc, np.uint8)
-    if restart:
+    if subsampling != 420:
+        n = orc().orc_encode_rgb_ex(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), int(restart), int(subsampling),
+                                    _p(out), cap)
+    elif restart:
         n = orc().orc_encode_rgb_restart(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), int(restart), _p(out), cap)
     else:
         n = orc().orc_encode_rgb(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), _p(out), cap)
@@ -113,6 +121,15 @@ def stage_coeffs(rgb: np.ndarray, quality: int = 50, maxval: int = 255):
     cr = np.zeros_like(cb)
     orc().orc_stage_coeffs(_p(rgb), w, h, maxval, _p(qy), _p(qc), _p(y), _p(cb), _p(cr))
     return y, cb, cr
+
+
+def stage_coeffs444(rgb: np.ndarray, quality: int = 50, maxval: int = 255):
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    qy, qc = quality_tables(quality)
+    planes = [np.zeros((((w + 7) // 8) * ((h + 7) // 8), 64), np.int16) for _ in range(3)]
+    orc().orc_stage_coeffs444(_p(rgb), w, h, maxval, _p(qy), _p(qc), *(_p(p) for p in planes))
+    return tuple(planes)
 
 
 def stage_hist(rgb: np.ndarray, quality: int = 50, maxval: int = 255):

@@ -236,3 +236,53 @@ def test_oracle_restart_variant_decodes_to_reference_pixels(w, h, r):
     a = np.asarray(Image.open(io.BytesIO(plain)).convert("RGB"))
     b = np.asarray(Image.open(io.BytesIO(rst)).convert("RGB"))
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("w,h", [(8, 8), (17, 9), (96, 80), (333, 211)])
+def test_oracle_s444_luma_equals_s420_luma(w, h):
+    # S444 changes only the chroma: the Y plane's coefficients are the S420_m path's
+    # (pinned to the reference), cropped to whole 8x8 blocks.
+    import jpgenc_amd as J
+    rgb = J.synth_rgb8(w + 5 * h, w, h, kind=1)
+    y420, _, _ = _oracle.stage_coeffs(rgb, 90)
+    y444, cb, cr = _oracle.stage_coeffs444(rgb, 90)
+    bw16, bw8, bh8 = (w + 15) // 16 * 2, (w + 7) // 8, (h + 7) // 8
+    crop = y420.reshape(-1, bw16, 64)[:bh8, :bw8].reshape(-1, 64)
+    assert np.array_equal(y444, crop)
+    assert cb.shape == cr.shape == y444.shape
+
+
+def test_oracle_s444_flat_chroma():
+    # a flat frame: every chroma block is DC-only, DC = round(8 * c / q0) with c the
+    # exact colour value (8 * c is the Arai DC of a constant block)
+    rgb = np.zeros((24, 40, 3), np.uint8)
+    rgb[...] = (200, 30, 90)
+    _, cb, cr = _oracle.stage_coeffs444(rgb, 50)
+    qy, qc = _oracle.quality_tables(50)
+    c = {"cb": -.1687 * 200 - .3312 * 30 + .5 * 90, "cr": .5 * 200 - .4186 * 30 - .0813 * 90}
+    for name, plane in (("cb", cb), ("cr", cr)):
+        assert np.all(plane[:, 1:] == 0)
+        assert np.all(plane[:, 0] == int(np.round(8 * c[name] / qc[0])))
+
+
+@pytest.mark.parametrize("w,h,r", [(8, 8, 0), (17, 33, 0), (96, 80, 0), (333, 211, 0), (64, 48, 1), (200, 136, 7)])
+def test_oracle_s444_decodes(w, h, r):
+    # The S444 variant is a valid baseline JPEG with 1x1 sampling everywhere: it
+    # decodes at full chroma resolution, closer to the input than the 4:2:0 stream.
+    Image = pytest.importorskip("PIL.Image")
+    import io
+
+    import jpgenc_amd as J
+    rgb = J.synth_rgb8(w * 3 + h, w, h)
+    data = _oracle.encode(rgb, 90, restart=r, subsampling=444)
+    sof = data.index(b"\xff\xc0")
+    assert data[sof + 10:sof + 19] == bytes([1, 0x11, 0, 2, 0x11, 1, 3, 0x11, 1])
+    assert (b"\xff\xdd" in data) == bool(r)
+    im = Image.open(io.BytesIO(data))
+    im.load()
+    assert im.size == (w, h)
+    dec = np.asarray(im.convert("RGB"), np.float64)
+    d420 = np.asarray(Image.open(io.BytesIO(_oracle.encode(rgb, 90))).convert("RGB"), np.float64)
+    mse444, mse420 = np.mean((dec - rgb) ** 2), np.mean((d420 - rgb) ** 2)
+    assert 10 * np.log10(255 ** 2 / mse444) > 30
+    assert mse444 <= mse420 * 1.05
