@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--restart", type=int, default=None,
                     help="restart interval in MCUs (16k-striped: default 1024 = one interval per MCU row, "
                          "the config's 'tiled with restart intervals'; 0 = the reference's single interval)")
+    ap.add_argument("--subsampling", type=int, choices=[420, 444], default=420,
+                    help="4k-frames: chroma subsampling (420 = the reference's S420_m; 444 = the S444 extension)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
@@ -121,7 +123,7 @@ def cpu_baseline(args) -> dict:
     for i in range(16):
         rgb = J.synth_rgb8(frame_seed(0, i), args.width, args.height)
         s = time.perf_counter()
-        _oracle.encode(rgb, args.quality)
+        _oracle.encode(rgb, args.quality, subsampling=args.subsampling)
         enc_times.append(time.perf_counter() - s)
         if sum(enc_times) >= args.cpu_seconds:
             break
@@ -131,10 +133,14 @@ def cpu_baseline(args) -> dict:
         "unit": "MPix/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{len(enc_times)} x {args.width}x{args.height} 4:2:0 Q{args.quality} frames (seeds 3..), "
+        "sample": f"{len(enc_times)} x {args.width}x{args.height} {sub_name(args)} Q{args.quality} frames (seeds 3..), "
                   f"oracle/jpge_oracle.cpp restatement, OpenMP {threads} threads (DCT/quant parallel, "
                   f"like the reference)",
     }
+
+
+def sub_name(args) -> str:
+    return "4:4:4" if getattr(args, "subsampling", 420) == 444 else "4:2:0"
 
 
 def cgroup_cpu_stat() -> dict:
@@ -317,6 +323,7 @@ def main():
 
     torch.cuda.set_device(local)
     enc = J.Encoder(local, lanes=args.lanes)
+    enc.set_subsampling(args.subsampling)
     W, H, F = args.width, args.height, args.frames
     pitch = W * 3
     cap = J.max_jpeg_bytes(W, H)
@@ -382,6 +389,7 @@ def main():
     solo_win = None
     if args.solo_batches > 0 and not args.no_kernel_events:
         solo = J.Encoder(local, lanes=1)
+        solo.set_subsampling(args.subsampling)
         solo.encode_batch_dev(frames, outd, quality=args.quality)
         solo.set_timing(1)
         solo.reset_timing()
@@ -395,11 +403,12 @@ def main():
     # per-kernel rooflines (HBM-bound integer/fp64 work; algorithmic bytes per launch)
     npx = W * H
     avg_jpeg = total_bytes / (args.steps * F)
-    traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H)
+    traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H) if args.subsampling == 420 else {}
+    cb = 6.0 if args.subsampling == 444 else 3.0  # coefficient bytes per pixel (3 or 1.5 int16)
     alg = {
-        "fdct_kernel": (6.0 * npx, "RGB8 read 3 B/px + int16 coefficients written 3 B/px"),
-        "stats_kernel": (3.0 * npx, "coefficients read 3 B/px"),
-        "entropy_kernel": (3.0 * npx + avg_jpeg, "coefficients read 3 B/px + entropy-coded bytes written"),
+        "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
+        "stats_kernel": (cb * npx, f"coefficients read {cb:g} B/px"),
+        "entropy_kernel": (cb * npx + avg_jpeg, f"coefficients read {cb:g} B/px + entropy-coded bytes written"),
     }
 
     def rooflines(tm):
@@ -427,7 +436,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "MPixels/s encode (4K 4:2:0 Q=90)",
+            "metric": f"MPixels/s encode (4K {sub_name(args)} Q=90)",
             "value": round(value, 1),
             "unit": "MPix/s",
             "n_gpus": world,
@@ -440,9 +449,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 photo-like frames, HBM-resident)",
             "config": {
-                "workload": f"{W}x{H} 4:2:0 Q{args.quality} full encode (RGB8 in HBM -> .jpg bytes in HBM), "
+                "workload": f"{W}x{H} {sub_name(args)} Q{args.quality} full encode (RGB8 in HBM -> .jpg bytes in HBM), "
                             f"{F} distinct frames per GPU per step",
-                "width": W, "height": H, "quality": args.quality, "subsampling": "4:2:0",
+                "width": W, "height": H, "quality": args.quality, "subsampling": sub_name(args),
                 "frames_per_step_per_gpu": F,
                 "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
                 "avg_jpeg_bytes": int(total_bytes / (args.steps * F)),

@@ -18,9 +18,11 @@ ap.add_argument("--quality", type=int, default=90)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--kind", type=int, default=0)
 ap.add_argument("--frames", type=int, default=1, help="distinct HBM-resident frames, encoded in turn")
+ap.add_argument("--subsampling", type=int, default=420, choices=[420, 444])
 a = ap.parse_args()
 
 enc = J.Encoder(0)
+enc.set_subsampling(a.subsampling)
 devs = [torch.from_numpy(J.synth_rgb8(3 + i, a.width, a.height, a.kind).reshape(-1)).cuda() for i in range(a.frames)]
 cap = J.max_jpeg_bytes(a.width, a.height)
 out = torch.empty(cap, dtype=torch.uint8, device="cuda")
