@@ -321,6 +321,44 @@ void subsample420m(const std::vector<double>& in, int W, int H, std::vector<doub
         }
 }
 
+// Image::subsample, Image.cpp:198-235, for every mask applySubsampling builds
+// (Image.cpp:256-309): mask row m of a scanline, summed from 0 in mask order; with
+// averaging the next scanline's sum is added and the result divided by 4 (S420_m)
+// or 2; without scanline_jump and without averaging every scanline is visited
+// (the --y at :229).  mode: 422 S422, 411 S411, 4200 S420, 4201 S420_lm, 420 S420_m,
+// 444 S444 (identity, :257-261).
+void subsample_mode(const std::vector<double>& chan, int W, int H, int mode, std::vector<double>& out) {
+    std::vector<uint8_t> row;
+    bool jump = false, averaging = false;
+    int vdiv = 2, hdiv = 2;
+    switch (mode) {
+        case 422: row = {1, 0}; vdiv = 1; hdiv = 2; break;
+        case 411: row = {1, 0, 0, 0}; vdiv = 1; hdiv = 4; break;
+        case 4200: row = {1, 0}; jump = true; break;
+        case 420: row = {1, 1}; averaging = true; break;
+        case 4201: row = {1, 0}; averaging = true; break;
+        default: out = chan; return;
+    }
+    const int rs = (int)row.size();
+    out.assign((size_t)(H / vdiv) * (W / hdiv), 0);
+    size_t idx = 0, idx2 = 0;
+    for (int y = 0; y < H;) {
+        for (int x = 0; x < W; x += rs) {
+            double v = 0;
+            for (int m = 0; m < rs; ++m) v += row[m] * chan[(size_t)y * W + x + m];
+            out[idx++] = v;
+        }
+        if (!jump && averaging) {
+            for (int x = 0; x < W; x += rs) {
+                double v = 0;
+                for (int m = 0; m < rs; ++m) v += row[m] * chan[(size_t)(y + 1) * W + x + m];
+                (out[idx2++] += v) /= (mode == 420 ? 4 : 2);
+            }
+        }
+        y += (!jump && !averaging) ? 1 : 2;  // y += 2 after the --y of :229
+    }
+}
+
 void dct_plane(const std::vector<double>& in, int W, int H, std::vector<double>& out) {
     out.assign((size_t)W * H, 0);
 #pragma omp parallel for schedule(static)
@@ -446,6 +484,80 @@ void dc_diff444(Frame& f, int R) {
         }
 }
 
+// Sampling shape of a subsampling mode: Y blocks across (yh) and down (yv) an MCU;
+// one Cb and one Cr block per MCU in every mode.
+bool mode_shape(int mode, int& yh, int& yv) {
+    switch (mode) {
+        case 420: case 4200: case 4201: yh = 2; yv = 2; return true;
+        case 444: yh = 1; yv = 1; return true;
+        case 422: yh = 2; yv = 1; return true;
+        case 411: yh = 4; yv = 1; return true;
+        default: return false;
+    }
+}
+
+// Generic subsampling-mode path (the modes of applySubsampling, Image.cpp:237-319,
+// that writeJPEG cannot emit).  At 420 and 444 it reproduces the
+// pinned paths above (a CPU test checks this).  The planes are edge-replicated to
+// whole MCUs of 8yh x 8yv px (Image.cpp:480-531 replicates to 16 px; 4:1:1 needs 32
+// across), converted (to_ycc), chroma-subsampled (subsample_mode), transformed and
+// quantised.
+void run_to_quant_mode(Frame& f, const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy,
+                       const uint8_t* qc, int mode) {
+    int yh, yv;
+    mode_shape(mode, yh, yv);
+    load_planes(f, rgb, w, h, maxval);
+    to_ycc(f);
+    f.R.clear(); f.G.clear(); f.B.clear();
+    const int MW = 8 * yh, MH = 8 * yv;
+    const int W = (w + MW - 1) / MW * MW, H = (h + MH - 1) / MH * MH;
+    for (std::vector<double>* p : {&f.Y, &f.Cb, &f.Cr}) {
+        std::vector<double> o((size_t)W * H);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x)
+                o[(size_t)y * W + x] = (*p)[(size_t)std::min(y, f.H - 1) * f.W + std::min(x, f.W - 1)];
+        p->swap(o);
+    }
+    f.W = W; f.H = H;
+    f.sw = W / yh; f.sh = H / yv;
+    std::vector<double> cb, cr;
+    subsample_mode(f.Cr, W, H, mode, cr);
+    subsample_mode(f.Cb, W, H, mode, cb);
+    f.Cb.swap(cb); f.Cr.swap(cr);
+    dct_plane(f.Y, W, H, f.dY);
+    dct_plane(f.Cb, f.sw, f.sh, f.dCb);
+    dct_plane(f.Cr, f.sw, f.sh, f.dCr);
+    quant_plane(f.dY, W, H, qy, f.qY);
+    quant_plane(f.dCb, f.sw, f.sh, qc, f.qCb);
+    quant_plane(f.dCr, f.sw, f.sh, qc, f.qCr);
+}
+
+// The Y block (v, u) of MCU (i, j), u across, v down, in a plane of W px.
+inline size_t y_block_origin(const Frame& f, int yh, int yv, int i, int j, int v, int u) {
+    return (size_t)((i * yv + v) * 8) * f.W + (size_t)(j * yh + u) * 8;
+}
+
+// DC chains (Image.cpp:638-678) in MCU order: Y over the MCU's yh*yv blocks row by
+// row (the MCU-order chain of :640-659), Cb and Cr over their blocks, whose raster
+// order is MCU order in every mode; restart R > 0 resets the three at the first MCU
+// of every interval.
+void dc_diff_mode(Frame& f, int yh, int yv, int R) {
+    int b[3] = {0, 0, 0}, m = 0;
+    for (int i = 0; i < f.sh / 8; ++i)
+        for (int j = 0; j < f.sw / 8; ++j, ++m) {
+            if (R && m % R == 0) b[0] = b[1] = b[2] = 0;
+            for (int v = 0; v < yv; ++v)
+                for (int u = 0; u < yh; ++u) {
+                    int& x = f.qY[y_block_origin(f, yh, yv, i, j, v, u)];
+                    int t = x; x = t - b[0]; b[0] = t;
+                }
+            for (int c = 1; c < 3; ++c) {
+                int& x = (c == 1 ? f.qCb : f.qCr)[(size_t)(i * 8) * f.sw + j * 8];
+                int t = x; x = t - b[c]; b[c] = t;
+            }
+        }
+}
+
 void block_syms(const std::vector<int>& plane, int W, int H, std::vector<std::vector<Sym>>& out) {
     int bw = W / 8, bh = H / 8;
     out.assign((size_t)bw * bh, {});
@@ -462,7 +574,7 @@ void put_u16(std::vector<uint8_t>& o, int v) { o.push_back((uint8_t)(v >> 8)); o
 
 // JFIF segments, JpegSegments.hpp:55-377 as used by Image.cpp:933-972.
 void write_headers(std::vector<uint8_t>& o, int rw, int rh, const uint8_t qy[64], const uint8_t qc[64],
-                   const Table* t[4], int restart = 0, bool s444 = false) {
+                   const Table* t[4], int restart = 0, uint8_t ysamp = 0x22) {
     const uint8_t soi_app0[] = {0xFF, 0xD8, 0xFF, 0xE0, 0, 16, 'J', 'F', 'I', 'F', 0, 1, 1, 0, 0, 1, 0, 1, 0, 0};
     o.insert(o.end(), soi_app0, soi_app0 + sizeof(soi_app0));
     const uint8_t* qt[2] = {qy, qc};
@@ -472,7 +584,7 @@ void write_headers(std::vector<uint8_t>& o, int rw, int rh, const uint8_t qy[64]
     }
     o.push_back(0xFF); o.push_back(0xC0); put_u16(o, 17); o.push_back(8);
     put_u16(o, rh & 0xFFFF); put_u16(o, rw & 0xFFFF); o.push_back(3);
-    const uint8_t comp[9] = {1, (uint8_t)(s444 ? 0x11 : 0x22), 0, 2, 0x11, 1, 3, 0x11, 1};
+    const uint8_t comp[9] = {1, ysamp, 0, 2, 0x11, 1, 3, 0x11, 1};  // Y: (H << 4) | V sampling factors
     o.insert(o.end(), comp, comp + 9);
     const uint8_t info[4] = {0x00, 0x10, 0x01, 0x11};
     for (int k = 0; k < 4; ++k) {
@@ -527,7 +639,7 @@ int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy
     Table tyd = build_table(ydc), tya = build_table(yac), tcd = build_table(cdc), tca = build_table(cac);
     const Table* tabs[4] = {&tyd, &tya, &tcd, &tca};
     out.clear();
-    write_headers(out, f.rw, f.rh, qy, qc, tabs, restart, s444);
+    write_headers(out, f.rw, f.rh, qy, qc, tabs, restart, s444 ? 0x11 : 0x22);
     // MCU interleave, Image.cpp:957-968 (at 4:4:4 one block of each component)
     BitWriter bw;
     int ybw = f.W / 8, cbw = f.sw / 8, cbh = f.sh / 8;
@@ -548,6 +660,52 @@ int encode_frame(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy
                 emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j], tyd, tya);
                 emit_block(bw, sY[(size_t)(2 * i + 1) * ybw + 2 * j + 1], tyd, tya);
             }
+            emit_block(bw, sCb[(size_t)i * cbw + j], tcd, tca);
+            emit_block(bw, sCr[(size_t)i * cbw + j], tcd, tca);
+        }
+    bw.fill();
+    bw.stuff_into(out);
+    out.push_back(0xFF); out.push_back(0xD9);
+    return 0;
+}
+
+// The generic subsampling-mode encode (run_to_quant_mode / dc_diff_mode): texts in
+// block raster order per component (Image.cpp:888-906), MCUs of yh*yv Y blocks
+// (row by row) + Cb + Cr (the interleave of Image.cpp:957-968 generalised), SOF0
+// declaring Y as yh x yv.
+int encode_frame_mode(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                      std::vector<uint8_t>& out, int restart, int mode) {
+    int yh, yv;
+    if (!mode_shape(mode, yh, yv)) return -1;
+    if (w <= 0 || h <= 0 || maxval <= 0 || maxval > 255 || restart < 0 || restart > 65535) return -1;
+    Frame f;
+    run_to_quant_mode(f, rgb, w, h, maxval, qy, qc, mode);
+    dc_diff_mode(f, yh, yv, restart);
+    std::vector<std::vector<Sym>> sY, sCb, sCr;
+    block_syms(f.qY, f.W, f.H, sY);
+    block_syms(f.qCb, f.sw, f.sh, sCb);
+    block_syms(f.qCr, f.sw, f.sh, sCr);
+    std::vector<int> ydc, yac, cdc, cac;
+    for (auto& b : sY) { ydc.push_back(b[0].symbol); for (size_t i = 1; i < b.size(); ++i) yac.push_back(b[i].symbol); }
+    for (auto* pl : {&sCb, &sCr})
+        for (auto& b : *pl) { cdc.push_back(b[0].symbol); for (size_t i = 1; i < b.size(); ++i) cac.push_back(b[i].symbol); }
+    Table tyd = build_table(ydc), tya = build_table(yac), tcd = build_table(cdc), tca = build_table(cac);
+    const Table* tabs[4] = {&tyd, &tya, &tcd, &tca};
+    out.clear();
+    write_headers(out, f.rw, f.rh, qy, qc, tabs, restart, (uint8_t)((yh << 4) | yv));
+    BitWriter bw;
+    const int ybw = f.W / 8, cbw = f.sw / 8, cbh = f.sh / 8;
+    int mcu = 0;
+    for (int i = 0; i < cbh; ++i)
+        for (int j = 0; j < cbw; ++j, ++mcu) {
+            if (restart && mcu > 0 && mcu % restart == 0) {
+                bw.fill();
+                bw.stuff_into(out);
+                out.push_back(0xFF); out.push_back((uint8_t)(0xD0 + ((mcu / restart - 1) & 7)));
+                bw = BitWriter();
+            }
+            for (int v = 0; v < yv; ++v)
+                for (int u = 0; u < yh; ++u) emit_block(bw, sY[(size_t)(i * yv + v) * ybw + j * yh + u], tyd, tya);
             emit_block(bw, sCb[(size_t)i * cbw + j], tcd, tca);
             emit_block(bw, sCr[(size_t)i * cbw + j], tcd, tca);
         }
@@ -764,15 +922,57 @@ int64_t orc_encode_rgb_restart(const uint8_t* rgb, int w, int h, int maxval, con
     return (int64_t)o.size();
 }
 
-// Either variant: restart MCUs per interval (0 = none), subsampling 420 or 444.
-int64_t orc_encode_rgb_ex(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
-                          int restart, int subsampling, uint8_t* out, int64_t cap) {
-    if (subsampling != 420 && subsampling != 444) return -1;
+// Any variant: restart MCUs per interval (0 = none); subsampling 420 (S420_m) or 444
+// through the pinned paths, 422 / 411 / 4200 (S420) / 4201 (S420_lm) through the
+// generic one; generic = 1 forces the generic path (consistency tests).
+int64_t orc_encode_rgb_mode(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                            int restart, int subsampling, int generic, uint8_t* out, int64_t cap) {
+    int yh, yv;
+    if (!mode_shape(subsampling, yh, yv)) return -1;
     std::vector<uint8_t> o;
-    if (encode_frame(rgb, w, h, maxval, qy, qc, o, restart, subsampling == 444) != 0) return -1;
+    const bool pinned = !generic && (subsampling == 420 || subsampling == 444);
+    const int st = pinned ? encode_frame(rgb, w, h, maxval, qy, qc, o, restart, subsampling == 444)
+                          : encode_frame_mode(rgb, w, h, maxval, qy, qc, o, restart, subsampling);
+    if (st != 0) return -1;
     if ((int64_t)o.size() > cap) return -(int64_t)o.size();
     memcpy(out, o.data(), o.size());
     return (int64_t)o.size();
+}
+
+int64_t orc_encode_rgb_ex(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                          int restart, int subsampling, uint8_t* out, int64_t cap) {
+    return orc_encode_rgb_mode(rgb, w, h, maxval, qy, qc, restart, subsampling, 0, out, cap);
+}
+
+// Stage dump of the generic path: quantised coefficients before DC differencing,
+// Y plane of ceil(w/8yh)*yh x ceil(h/8yv)*yv blocks and the two chroma planes of
+// ceil(w/8yh) x ceil(h/8yv) blocks, raster order, natural order inside a block.
+int orc_stage_coeffs_mode(const uint8_t* rgb, int w, int h, int maxval, const uint8_t* qy, const uint8_t* qc,
+                          int mode, int16_t* outY, int16_t* outCb, int16_t* outCr) {
+    int yh, yv;
+    if (!mode_shape(mode, yh, yv)) return -1;
+    Frame f;
+    run_to_quant_mode(f, rgb, w, h, maxval, qy, qc, mode);
+    auto dump = [](const std::vector<int>& pl, int W, int H, int16_t* o) {
+        const int bw = W / 8, bh = H / 8;
+        for (int by = 0; by < bh; ++by)
+            for (int bx = 0; bx < bw; ++bx)
+                for (int i = 0; i < 8; ++i)
+                    for (int j = 0; j < 8; ++j)
+                        o[((size_t)by * bw + bx) * 64 + i * 8 + j] = (int16_t)pl[(size_t)(by * 8 + i) * W + bx * 8 + j];
+    };
+    dump(f.qY, f.W, f.H, outY);
+    dump(f.qCb, f.sw, f.sh, outCb);
+    dump(f.qCr, f.sw, f.sh, outCr);
+    return 0;
+}
+
+// subsample_mode of an arbitrary W x H plane (Image::subsample for one mode).
+int orc_subsample_mode(const double* in, int W, int H, int mode, double* out) {
+    std::vector<double> v(in, in + (size_t)W * H), o;
+    subsample_mode(v, W, H, mode, o);
+    memcpy(out, o.data(), o.size() * 8);
+    return (int)o.size();
 }
 
 // Stage dump of the S444 variant: quantised coefficients before DC differencing,

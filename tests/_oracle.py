@@ -51,6 +51,10 @@ def orc() -> ctypes.CDLL:
         L.orc_encode_rgb_ex.restype = i64
         L.orc_encode_rgb_ex.argtypes = [vp, i32, i32, i32, vp, vp, i32, i32, vp, i64]
         L.orc_stage_coeffs444.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
+        L.orc_encode_rgb_mode.restype = i64
+        L.orc_encode_rgb_mode.argtypes = [vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, i64]
+        L.orc_stage_coeffs_mode.argtypes = [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp]
+        L.orc_subsample_mode.argtypes = [vp, i32, i32, i32, vp]
         L.orc_set_threads.argtypes = [i32]
         _orc = L
     return _orc
@@ -88,20 +92,25 @@ def huffman(text, lib=None, fn="orc_huffman"):
     return list(zip(s[:k].tolist(), ln[:k].tolist(), c[:k].tolist()))
 
 
+#: subsampling mode -> (Y blocks across, Y blocks down) an MCU (jpge.h JPGE_S*)
+SHAPES = {420: (2, 2), 4200: (2, 2), 4201: (2, 2), 444: (1, 1), 422: (2, 1), 411: (4, 1)}
+
+
 def encode(rgb: np.ndarray, quality: int = 50, maxval: int = 255, qy=None, qc=None, restart: int = 0,
-           subsampling: int = 420) -> bytes:
+           subsampling: int = 420, generic: bool = False) -> bytes:
     """writeJPEG; restart > 0: the restart-interval variant (DRI + RSTn every `restart` MCUs);
-    subsampling 444: the S444 variant."""
+    subsampling 444 / 422 / 411 / 4200 (S420) / 4201 (S420_lm): the subsampling variants;
+    generic: force the generic subsampling path (consistency checks at 420 / 444)."""
     rgb = np.ascontiguousarray(rgb, np.uint8)
     h, w = rgb.shape[:2]
     if qy is None:
         qy, qc = quality_tables(quality)
-    cap = 4096 + ((w + 7) // 8) * ((h + 7) // 8) * (3 * 420 + 4)
+    cap = 4096 + ((w + 31) // 8) * ((h + 15) // 8) * (3 * 420 + 4)
     out = np.empty(cap, np.uint8)
     qy8, qc8 = np.ascontiguousarray(qy, np.uint8), np.ascontiguousarray(qc, np.uint8)
-    if subsampling != 420:
-        n = orc().orc_encode_rgb_ex(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), int(restart), int(subsampling),
-                                    _p(out), cap)
+    if subsampling != 420 or generic:
+        n = orc().orc_encode_rgb_mode(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), int(restart), int(subsampling),
+                                      int(generic), _p(out), cap)
     elif restart:
         n = orc().orc_encode_rgb_restart(_p(rgb), w, h, maxval, _p(qy8), _p(qc8), int(restart), _p(out), cap)
     else:
@@ -130,6 +139,29 @@ def stage_coeffs444(rgb: np.ndarray, quality: int = 50, maxval: int = 255):
     planes = [np.zeros((((w + 7) // 8) * ((h + 7) // 8), 64), np.int16) for _ in range(3)]
     orc().orc_stage_coeffs444(_p(rgb), w, h, maxval, _p(qy), _p(qc), *(_p(p) for p in planes))
     return tuple(planes)
+
+
+def stage_coeffs_mode(rgb: np.ndarray, mode: int, quality: int = 50, maxval: int = 255):
+    """Quantised coefficients of the generic subsampling path (before DC differencing)."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    yh, yv = SHAPES[mode]
+    mw, mh = -(-w // (8 * yh)), -(-h // (8 * yv))
+    qy, qc = quality_tables(quality)
+    y = np.zeros((mw * yh * mh * yv, 64), np.int16)
+    cb = np.zeros((mw * mh, 64), np.int16)
+    cr = np.zeros_like(cb)
+    orc().orc_stage_coeffs_mode(_p(rgb), w, h, maxval, _p(qy), _p(qc), int(mode), _p(y), _p(cb), _p(cr))
+    return y, cb, cr
+
+
+def subsample_mode(plane: np.ndarray, mode: int) -> np.ndarray:
+    p = np.ascontiguousarray(plane, np.float64)
+    H, W = p.shape
+    yh, yv = SHAPES[mode]
+    out = np.zeros((H // yv) * (W // yh) if mode != 444 else H * W, np.float64)
+    orc().orc_subsample_mode(_p(p), W, H, int(mode), _p(out))
+    return out.reshape(H // yv, W // yh) if mode != 444 else out.reshape(H, W)
 
 
 def stage_hist(rgb: np.ndarray, quality: int = 50, maxval: int = 255):
