@@ -93,16 +93,26 @@ int jpge_get_lanes(jpge_ctx* ctx, int* lanes);
  * 1..65535, else JPGE_E_ARG; the stripe phases (jpge_stripe_*) need mcus = 0. */
 int jpge_set_restart_interval(jpge_ctx* ctx, uint32_t mcus);
 
-/* Chroma subsampling for the context's following encodes: 420 (the default:
- * applySubsampling(S420_m) as writeJPEG hard-codes it, Image.cpp:842, bit-identical
- * to the reference) or 444 (applySubsampling(S444), Image.cpp:257-261: no
- * subsampling; 8x8 MCUs of Y, Cb, Cr, all 1x1 in SOF0).  The reference's writeJPEG
- * cannot emit 4:4:4; the oracle's S444 variant pins the bytes.  Other modes:
- * JPGE_E_ARG.  jpge_fdct_quant then returns three full-resolution planes; the
- * stripe phases (jpge_stripe_*) need 420. */
+/* Subsampling modes: the SubsamplingMode enum of Image.hpp:44-52, as passed to
+ * Image::applySubsampling (Image.cpp:237-319). */
+#define JPGE_S420_M 420  /* mean of 2x2 (writeJPEG's mode; the default)        MCU 16x16, Y 2x2 */
+#define JPGE_S444 444    /* no subsampling                                    MCU  8x8,  Y 1x1 */
+#define JPGE_S422 422    /* every second pixel of a row                       MCU 16x8,  Y 2x1 */
+#define JPGE_S411 411    /* every fourth pixel of a row                       MCU 32x8,  Y 4x1 */
+#define JPGE_S420 4200   /* every second pixel of every second row            MCU 16x16, Y 2x2 */
+#define JPGE_S420_LM 4201 /* mean of the two rows' left pixels                MCU 16x16, Y 2x2 */
+
+/* Chroma subsampling for the context's following encodes.  JPGE_S420_M (the
+ * default) is applySubsampling(S420_m) as writeJPEG hard-codes it (Image.cpp:842),
+ * bit-identical to the reference.  The other modes follow Image::subsample
+ * (Image.cpp:198-235) for the masks of applySubsampling; writeJPEG cannot emit
+ * them, so the oracle's composition of the pinned stages defines their bytes: the
+ * frame edge-replicated to whole MCUs, MCU = the Y blocks row by row + Cb + Cr,
+ * SOF0 declaring Y as H x V.  Unknown modes: JPGE_E_ARG.  jpge_fdct_quant then
+ * returns the mode's planes; the stripe phases (jpge_stripe_*) need JPGE_S420_M. */
 int jpge_set_subsampling(jpge_ctx* ctx, int mode);
 
-/* Worst-case .jpg size for a frame, in either subsampling mode (header + 2x
+/* Worst-case .jpg size for a frame, in any subsampling mode (header + 2x
  * worst-case entropy + RST markers + EOI). */
 size_t jpge_max_jpeg_bytes(uint32_t width, uint32_t height);
 

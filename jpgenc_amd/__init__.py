@@ -22,6 +22,9 @@ LIB_PATH = os.environ.get("JPGE_LIB") or os.path.join(_HERE, "lib", "libjpge.so"
 JPGE_DEVICE_INPUT = 1
 JPGE_DEVICE_OUTPUT = 2
 
+#: subsampling modes (jpge.h JPGE_S*) -> (Y blocks across, Y blocks down) an MCU
+SUBSAMPLING = {420: (2, 2), 4200: (2, 2), 4201: (2, 2), 444: (1, 1), 422: (2, 1), 411: (4, 1)}
+
 STATUS = {
     0: "JPGE_OK", 1: "JPGE_E_ARG", 2: "JPGE_E_NOSPACE", 3: "JPGE_E_HIP", 4: "JPGE_E_NODEV",
     5: "JPGE_E_FORMAT", 6: "JPGE_E_IO", 7: "JPGE_E_TRUNC", 8: "JPGE_E_RANGE", 9: "JPGE_E_TIMEOUT",
@@ -282,8 +285,9 @@ class Encoder:
         _check(lib().jpge_set_restart_interval(self._ctx, int(mcus)), "set_restart_interval")
 
     def set_subsampling(self, mode: int) -> None:
-        """Chroma subsampling for the following encodes: 420 (the reference's S420_m, the
-        default) or 444 (S444: no subsampling, 8x8 MCUs)."""
+        """Chroma subsampling for the following encodes (applySubsampling's modes,
+        Image.hpp:44-52): 420 (S420_m, the reference's writeJPEG, the default), 444
+        (S444), 422 (S422), 411 (S411), 4200 (S420) or 4201 (S420_lm); see SUBSAMPLING."""
         _check(lib().jpge_set_subsampling(self._ctx, int(mode)), "set_subsampling")
         self._sub = int(mode)
 
@@ -347,13 +351,10 @@ class Encoder:
         (nblocks, 64), blocks in raster order, natural order within a block."""
         rgb = np.ascontiguousarray(rgb, np.uint8)
         h, w = rgb.shape[:2]
-        if getattr(self, "_sub", 420) == 444:
-            y = np.zeros((((w + 7) // 8) * ((h + 7) // 8), 64), np.int16)
-            cb = np.zeros_like(y)
-        else:
-            W, H = (w + 15) // 16 * 16, (h + 15) // 16 * 16
-            y = np.zeros(((W // 8) * (H // 8), 64), np.int16)
-            cb = np.zeros(((W // 16) * (H // 16), 64), np.int16)
+        yh, yv = SUBSAMPLING[getattr(self, "_sub", 420)]
+        mw, mh = -(-w // (8 * yh)), -(-h // (8 * yv))  # MCUs across / down
+        y = np.zeros((mw * yh * mh * yv, 64), np.int16)
+        cb = np.zeros((mw * mh, 64), np.int16)
         cr = np.zeros_like(cb)
         qy, qc = self._tables(quality, qy, qc)
         _check(lib().jpge_fdct_quant(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(y), _p(cb),

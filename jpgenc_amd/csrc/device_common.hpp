@@ -72,14 +72,15 @@ constexpr int kPartsPerBlock = 4;  // lanes cooperating on one block's non-zero 
 
 // DC predecessor of flat block g (Image.cpp:638-678): the Y chain runs in MCU
 // order, Cb and Cr each over their own blocks; a chain's first block predicts 0.
-// The predecessor is at most 6 blocks back.  At 4:4:4 (bpm 3) every chain runs in
-// MCU order: the predecessor is the same slot of the previous MCU.
+// The predecessor is at most 6 blocks back (bpm <= 6).  In every mode the Y chain
+// runs in MCU order over the MCU's bpm - 2 Y slots, so an MCU's first Y block
+// follows the previous MCU's last (3 blocks back: past Cr and Cb), and each chroma
+// block follows the same slot of the previous MCU.
 __device__ __forceinline__ int64_t dc_pred_index(uint64_t g, uint32_t bpm) {
-    if (bpm == 3) return g < 3 ? -1 : (int64_t)g - 3;
-    const int k = (int)(g % 6);
-    if (k >= 1 && k <= 3) return (int64_t)g - 1;
-    if (g < 6) return -1;
-    return (int64_t)g - (k == 0 ? 3 : 6);
+    const int k = (int)(g % bpm);
+    if (k >= 1 && k < (int)bpm - 2) return (int64_t)g - 1;
+    if (g < bpm) return -1;
+    return (int64_t)g - (k == 0 ? 3 : bpm);
 }
 
 // One tile of kBlocks coefficient blocks (natural order in HBM) held in registers

@@ -27,17 +27,30 @@ namespace jpge {
 
 namespace {
 
-// bpm 6: 4:2:0, 16x16 px MCUs; bpm 3: 4:4:4, 8x8 px MCUs (the frame cropped to whole
-// 8x8 blocks of the reference's 16-padded planes: the padding is edge replication
-// either way)
-inline Geometry geometry(uint32_t w, uint32_t h, uint32_t bpm = 6) {
+// MCU shape of a subsampling mode (jpge.h JPGE_S*): Y blocks across, blocks per MCU
+// and the 4:2:0 chroma filter; false for an unknown mode.
+bool mode_shape(int mode, uint32_t& yh, uint32_t& bpm, uint32_t& cfilt) {
+    cfilt = kFiltS420m;
+    switch (mode) {
+        case 420: yh = 2; bpm = 6; return true;
+        case 4201: yh = 2; bpm = 6; cfilt = kFiltS420lm; return true;
+        case 4200: yh = 2; bpm = 6; cfilt = kFiltS420; return true;
+        case 444: yh = 1; bpm = 3; return true;
+        case 422: yh = 2; bpm = 4; return true;
+        case 411: yh = 4; bpm = 6; return true;
+        default: return false;
+    }
+}
+
+// The frame in whole MCUs (4:2:0: 16x16 px, the reference's padding, Image.cpp:480-531;
+// the other modes pad to their own MCU size: edge replication either way)
+inline Geometry geometry(uint32_t w, uint32_t h, int mode = 420) {
     Geometry g;
     g.width = w;
     g.height = h;
-    g.bpm = bpm;
-    const uint32_t e = g.mcu_px();
-    g.mw = (w + e - 1) / e;
-    g.mh = (h + e - 1) / e;
+    mode_shape(mode, g.yh, g.bpm, g.cfilt);
+    g.mw = (w + g.mcu_w() - 1) / g.mcu_w();
+    g.mh = (h + g.mcu_h() - 1) / g.mcu_h();
     return g;
 }
 
@@ -306,8 +319,9 @@ int Encoder::set_restart(uint32_t mcus) {
 }
 
 int Encoder::set_subsampling(int mode) {
-    if (mode != 420 && mode != 444) return kErrArg;
-    bpm_ = mode == 444 ? 3u : 6u;
+    uint32_t yh, bpm, cf;
+    if (!mode_shape(mode, yh, bpm, cf)) return kErrArg;
+    mode_ = mode;
     return kOk;
 }
 
@@ -315,10 +329,10 @@ size_t Encoder::max_jpeg_bytes(uint32_t w, uint32_t h) {
     // header <= 20 + 2*69 + 19 + 4*(4+17+256) + 14 ; entropy <= 1665 bits/block,
     // doubled for worst-case 0xFF stuffing; + EOI.
     // Restart intervals add per MCU at most an RST marker, a fill byte and its stuffing.
-    // (The larger of the 4:2:0 and 4:4:4 bounds: one capacity serves either mode.)
+    // (The largest bound over the MCU shapes: one capacity serves every mode.)
     size_t cap = 0;
-    for (uint32_t bpm : {6u, 3u}) {
-        const Geometry g = geometry(w, h, bpm);
+    for (int mode : {420, 444, 422, 411}) {
+        const Geometry g = geometry(w, h, mode);
         cap = std::max(cap, 2048 + (size_t)g.nblocks() * 2 * 209 + 16 + (size_t)g.nmcu() * 4);
     }
     return cap;
@@ -522,7 +536,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
                     Slot* imp, bool export_hist) {
     if (!f.rgb || f.width == 0 || f.height == 0 || f.width > 65535 || f.height > 65535) return kErrArg;
     if (f.maxval < 1 || f.maxval > 255) return kErrRange;
-    const Geometry g = geometry(f.width, f.height, bpm_);
+    const Geometry g = geometry(f.width, f.height, mode_);
     const size_t row = (size_t)f.width * 3;
     const size_t stride = f.stride ? f.stride : row;
     if (stride < row) return kErrArg;
@@ -610,7 +624,8 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
     if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
-    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_, s.g.s444());
+    const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_,
+                                                    (uint8_t)((s.g.yh << 4) | s.g.yv()));
     if (hdr.size() > kHdrMax) return kErrInternal;
     std::memcpy(reinterpret_cast<uint8_t*>(s.h_tab) + kTabBytes, hdr.data(), hdr.size());
     s.hdr_len = hdr.size();
@@ -873,15 +888,14 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
     const Geometry& g = s.g;
     std::vector<int16_t> coef((size_t)g.nblocks() * 64);
     JPGE_HIP(hipMemcpy(coef.data(), s.d_coef, coef.size() * 2, hipMemcpyDeviceToHost));
-    const uint32_t ybw = (g.bpm == 3 ? 1 : 2) * g.mw, cbw = g.mw;
+    const uint32_t ybw = g.yh * g.mw, cbw = g.mw;
     for (uint32_t m = 0; m < g.nmcu(); ++m) {
         const uint32_t mr = m / g.mw, mc = m % g.mw;
         for (int k = 0; k < (int)g.bpm; ++k) {
             const int16_t* src = &coef[((size_t)m * g.bpm + k) * 64];
             const int comp = block_comp(k, g.bpm);
             int16_t* dst;
-            if (comp == 0 && g.bpm == 3) dst = y + (size_t)m * 64;
-            else if (comp == 0) dst = y + ((size_t)(2 * mr + (k >> 1)) * ybw + 2 * mc + (k & 1)) * 64;
+            if (comp == 0) dst = y + ((size_t)(mr * g.yv() + k / g.yh) * ybw + mc * g.yh + k % g.yh) * 64;
             else dst = (comp == 1 ? cb : cr) + ((size_t)mr * cbw + mc) * 64;
             for (int i = 0; i < 64; ++i) dst[i] = src[i];
         }
@@ -914,7 +928,7 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
 int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]) {
     JPGE_HIP(hipSetDevice(device_));
     if (!d.rgb || !last_dc || d.width == 0 || d.height == 0 || d.width > 65535 || d.height > 65535) return kErrArg;
-    if (bpm_ != 6) return kErrArg;  // stripes are 4:2:0 (the reference's subsampling)
+    if (mode_ != 420) return kErrArg;  // stripes are S420_m (the reference's subsampling)
     if (d.maxval < 1 || d.maxval > 255) return kErrRange;
     const uint32_t mh_img = (d.height + 15) / 16;
     if (d.mcu_rows == 0 || d.mcu_row0 >= mh_img || d.mcu_rows > mh_img - d.mcu_row0) return kErrArg;

@@ -89,10 +89,10 @@ class Encoder {
     // stream); not for the stripe phases
     int set_restart(uint32_t mcus);
     uint32_t restart() const { return restart_mcus_; }
-    // chroma subsampling of the following encodes: 420 (S420_m, the reference's
-    // writeJPEG) or 444 (no subsampling: 8x8 MCUs of Y, Cb, Cr); stripes are 420 only
+    // chroma subsampling of the following encodes (jpge.h JPGE_S*): 420 (S420_m, the
+    // reference's writeJPEG), 444, 422, 411, 4200 (S420), 4201 (S420_lm); stripes are 420 only
     int set_subsampling(int mode);
-    int subsampling() const { return bpm_ == 3 ? 444 : 420; }
+    int subsampling() const { return mode_; }
 
     int lanes() const { return (int)lanes_.size(); }
 
@@ -127,7 +127,7 @@ class Encoder {
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
-    uint32_t bpm_ = 6;          // blocks per MCU: 6 (4:2:0) or 3 (4:4:4) (jpge_set_subsampling)
+    int mode_ = 420;            // subsampling mode (jpge_set_subsampling)
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs_); }
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch

@@ -123,7 +123,13 @@ __device__ __forceinline__ double ycc_ref_c(uint32_t p, double scale, double kr,
     return (128.0 + ((kr * r + kg * g) + kb * b)) - 128;
 }
 
-template <bool kExact, int kWaves>
+// exact chroma of one 8-bit pixel: (128 + v) - 128 == v, v exact
+__device__ __forceinline__ double ycc_exact_c(uint32_t p, double kr, double kg, double kb) {
+    const double r = (double)(p & 0xFF), g = (double)((p >> 8) & 0xFF), b = (double)(p >> 16);
+    return __builtin_fma(kb, b, __builtin_fma(kg, g, kr * r));
+}
+
+template <bool kExact, int kWaves, int kFilt>
 __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     constexpr int kK1Threads = kWaves * 64;
     __shared__ K1Lds<kWaves> lds;
@@ -228,7 +234,23 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint2 t0 = c[2 * i], t1 = c[2 * i + 1];
-            if (kExact) {
+            if (kFilt == kFiltS420) {
+                // subsample(S420), Image.cpp:279-286: mask {1, 0} on even rows only, the
+                // top-left sample (the mask's 0 * b adds a zero)
+                x[i] = kExact ? ycc_exact_c(t0.x, kr, kg, kb) : ycc_ref_c(t0.x, scale, kr, kg, kb);
+            } else if (kFilt == kFiltS420lm) {
+                // subsample(S420_lm), Image.cpp:297-306, 218-224: (a + c) / 2 of the left
+                // samples of both rows; exact for 8-bit input, as the channel sums
+                if (kExact) {
+                    const uint32_t rb = (t0.x & 0xFF00FFu) + (t1.x & 0xFF00FFu), all = t0.x + t1.x;
+                    const double sr = (double)(rb & 0xFFFF), sb = (double)(rb >> 16), sg = (double)((all - rb) >> 8);
+                    x[i] = __builtin_fma(kb * 0.5, sb, __builtin_fma(kg * 0.5, sg, (kr * 0.5) * sr));
+                } else {
+                    double v = ycc_ref_c(t0.x, scale, kr, kg, kb);
+                    v += ycc_ref_c(t1.x, scale, kr, kg, kb);
+                    x[i] = v / 2;
+                }
+            } else if (kExact) {
                 // ((a+b)+(c+d))/4 of the exact per-pixel values equals the exact value
                 // of the channel sums
                 const uint32_t rb = (t0.x & 0xFF00FFu) + (t0.y & 0xFF00FFu) + (t1.x & 0xFF00FFu) + (t1.y & 0xFF00FFu);
@@ -364,30 +386,31 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     JPGE_STAMP(7);
 }
 
-// ---- 4:4:4 (S444 extension: applySubsampling(S444), Image.cpp:257-261, is the
-// identity; MCU = one 8x8 block of each of Y, Cb, Cr) ----
-// Same machinery as fdct_kernel: a wave owns a tile of 16 MCUs (128x8 px; a lane
-// stages one 16-px run of one row), in six rounds of 8 blocks: Y MCUs 0-7, Y MCUs
-// 8-15, Cb 0-7, Cb 8-15, Cr 0-7, Cr 8-15 (lane = (block of the round, column)).
-// Chroma is converted per pixel: for 8-bit input (128 + v) - 128 == v exactly, and
-// v = fma(kb, b, fma(kg, g, kr r)) is exact.
+// ---- MCUs one block row high: 4:4:4, 4:2:2, 4:1:1 (applySubsampling S444, S422,
+// S411, Image.cpp:257-278; the MCU is kYh Y blocks across + Cb + Cr) ----
+// Same machinery as fdct_kernel: a wave owns a tile of 128x8 px (16 Y blocks,
+// 16 / kYh MCUs; a lane stages one 16-px run of one row), in rounds of 8 blocks
+// (lane = (block of the round, column)): Y blocks 0-7, Y blocks 8-15, then the
+// chroma blocks — 4:4:4: Cb 0-7, Cb 8-15, Cr 0-7, Cr 8-15; 4:2:2: Cb 0-7, Cr 0-7;
+// 4:1:1: Cb 0-3 + Cr 0-3 in one round.  S422 / S411 keep the first sample of each
+// 2 / 4 along a row (mask {1,0} / {1,0,0,0}, every scanline; the mask's zero terms
+// add zeros).  Chroma is converted per pixel: for 8-bit input (128 + v) - 128 == v
+// exactly, and v = fma(kb, b, fma(kg, g, kr r)) is exact.
 constexpr int kRgbPitch444 = 130;  // u32 per staged row of 128 px (+2: even, for uint2 stores)
 static_assert(8 * kRgbPitch444 <= 16 * kRgbPitch, "the 4:4:4 tile fits the 4:2:0 staging area");
 
-__device__ __forceinline__ double ycc_exact_c(uint32_t p, double kr, double kg, double kb) {
-    const double r = (double)(p & 0xFF), g = (double)((p >> 8) & 0xFF), b = (double)(p >> 16);
-    return __builtin_fma(kb, b, __builtin_fma(kg, g, kr * r));
-}
-
-template <bool kExact, int kWaves>
-__global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
+template <bool kExact, int kWaves, int kYh>
+__global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
     constexpr int kK1Threads = kWaves * 64;
+    constexpr uint32_t kMcus = 16 / kYh;            // MCUs per tile
+    constexpr int kBpm = kYh + 2;                   // blocks per MCU
+    constexpr int kRounds = 2 + 4 / kYh;            // 2 Y rounds + the chroma rounds
     __shared__ K1Lds<kWaves> lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     K1WaveLds& W = lds.w[wv];
     JPGE_STAMP(1);
     const uint32_t mw = a.g.mw;
-    const uint32_t tiles_per_row = (mw + 15) / 16;
+    const uint32_t tiles_per_row = (mw + kMcus - 1) / kMcus;
     const uint32_t ntiles = tiles_per_row * a.g.mh;
     const double scale = 255.0 / (double)a.maxval;  // Image.cpp:465
     const bool aligned = (((uintptr_t)a.rgb | a.stride) & 15) == 0;
@@ -410,8 +433,8 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
     };
     auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
         const uint32_t t = tb_p + k;
-        const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * 16;
-        const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 + c8 * 16;
+        const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * kMcus;
+        const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 * kYh + c8 * 16;
         const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
         const uint32_t off = ok ? (uint32_t)((uint64_t)y * a.stride + (uint64_t)xs * 3) : kOob;
         v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
@@ -442,7 +465,10 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
 
     double* tb = &W.tmp[b8 * kTmpBlock];
     auto load_px = [&](int round, uint32_t p[8]) {  // column j of the round's block b8
-        const int col = ((round & 1) * 8 + b8) * 8 + j;
+        int col;
+        if (round < 2 || kYh == 1) col = ((round & 1) * 8 + b8) * 8 + j;  // full resolution
+        else if (kYh == 2) col = b8 * 16 + 2 * j;                          // S422: left of each pair
+        else col = (b8 & 3) * 32 + 4 * j;                                  // S411: first of each 4
 #pragma unroll
         for (int i = 0; i < 8; ++i) p[i] = W.rgbx[i * kRgbPitch444 + col];
     };
@@ -454,9 +480,9 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
     for (; k < n_p;) {
         const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row;
-        const uint32_t mcol0 = (t % tiles_per_row) * 16;
-        const int nvalid = (int)min(16u, mw - mcol0);
-        const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 + c8 * 16;
+        const uint32_t mcol0 = (t % tiles_per_row) * kMcus;
+        const int nvalid = (int)min(kMcus, mw - mcol0);
+        const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 * kYh + c8 * 16;
 
         uint32_t px[16];
         {
@@ -491,8 +517,18 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
         load_iq(0, iq);
         wave_order();
 #pragma unroll
-        for (int round = 0; round < 6; ++round) {
-            const int comp = round >> 1, m = (round & 1) * 8 + b8, qb = comp ? 1 : 0;
+        for (int round = 0; round < kRounds; ++round) {
+            // the lane's block: component, MCU of the tile, slot in the MCU
+            int comp, m, slot;
+            if (round < 2) {
+                const int bx = round * 8 + b8;  // Y block of the tile
+                comp = 0; m = bx / kYh; slot = bx % kYh;
+            } else {
+                comp = kYh == 1 ? 1 + ((round - 2) >> 1) : kYh == 2 ? round - 1 : 1 + (b8 >> 2);
+                m = kYh == 1 ? (round & 1) * 8 + b8 : kYh == 2 ? b8 : (b8 & 3);
+                slot = kYh + comp - 1;
+            }
+            const int qb = comp ? 1 : 0;
             double x[8];
             if (comp == 0) {
 #pragma unroll
@@ -514,7 +550,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) iqc[u] = iq[u];
             wave_order();
-            if (round + 1 < 6) {  // the next round's inputs, after this round's LDS reads
+            if (round + 1 < kRounds) {  // the next round's inputs, after this round's LDS reads
                 load_px(round + 1, p);
                 if (round == 1) load_iq(1, iq);
             }
@@ -527,14 +563,14 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], kS[u], lds.q[qb][j * kQRow + u]);
             }
-            const uint32_t blk = (mrow * mw + mcol0 + m) * 3 + comp;
+            const uint32_t blk = (mrow * mw + mcol0 + m) * kBpm + slot;
             const uint32_t off = m < nvalid ? blk * 128 + j * 16 : kOob;
             u32x4 pk;
             pk.x = __builtin_amdgcn_perm((uint32_t)qv[1], (uint32_t)qv[0], 0x05040100u);
             pk.y = __builtin_amdgcn_perm((uint32_t)qv[3], (uint32_t)qv[2], 0x05040100u);
             pk.z = __builtin_amdgcn_perm((uint32_t)qv[5], (uint32_t)qv[4], 0x05040100u);
             pk.w = __builtin_amdgcn_perm((uint32_t)qv[7], (uint32_t)qv[6], 0x05040100u);
-            if (round < 5) {
+            if (round < kRounds - 1) {
                 __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
             } else {
                 pend = pk;
@@ -552,8 +588,33 @@ __global__ __launch_bounds__(kWaves * 64) void fdct444_kernel(FdctArgs a) {
 
 }  // namespace
 
+template <int kYh>
+void launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s) {
+    const bool ex = a.maxval == 255;
+    if (a.solo) {
+        if (ex) hipLaunchKernelGGL((fdct_row8_kernel<true, kK1WavesSolo, kYh>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+        else hipLaunchKernelGGL((fdct_row8_kernel<false, kK1WavesSolo, kYh>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+    } else {
+        if (ex) hipLaunchKernelGGL((fdct_row8_kernel<true, kK1WavesShared, kYh>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        else hipLaunchKernelGGL((fdct_row8_kernel<false, kK1WavesShared, kYh>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+    }
+}
+
+template <int kFilt>
+void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s) {
+    const bool ex = a.maxval == 255;
+    if (a.solo) {
+        if (ex) hipLaunchKernelGGL((fdct_kernel<true, kK1WavesSolo, kFilt>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+        else hipLaunchKernelGGL((fdct_kernel<false, kK1WavesSolo, kFilt>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+    } else {
+        if (ex) hipLaunchKernelGGL((fdct_kernel<true, kK1WavesShared, kFilt>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        else hipLaunchKernelGGL((fdct_kernel<false, kK1WavesShared, kFilt>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+    }
+}
+
 uint32_t fdct_grid(const Geometry& g, bool solo) {
-    const uint32_t tiles = ((g.mw + (g.s444() ? 15 : 3)) / (g.s444() ? 16 : 4)) * g.mh;
+    const uint32_t per = g.row8() ? 16 / g.yh : 4;  // MCUs per tile
+    const uint32_t tiles = ((g.mw + per - 1) / per) * g.mh;
     // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
     const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
     const uint32_t cap = solo ? 256u : 1024u;
@@ -565,27 +626,22 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
     // (a 16384^2 frame needs 805 MB of each)
     if ((uint64_t)a.stride * a.g.height >= kOob || (uint64_t)a.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
     const uint32_t grid = fdct_grid(a.g, a.solo);
-    if (a.g.s444()) {
-        const bool ex = a.maxval == 255;
-        if (a.solo) {
-            if (ex) hipLaunchKernelGGL((fdct444_kernel<true, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
-            else hipLaunchKernelGGL((fdct444_kernel<false, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
-        } else {
-            if (ex) hipLaunchKernelGGL((fdct444_kernel<true, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
-            else hipLaunchKernelGGL((fdct444_kernel<false, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+    // the kernels assume these shapes (kernels.hpp Geometry)
+    if (a.g.row8()) {
+        switch (a.g.yh) {
+            case 1: if (a.g.bpm != 3) return hipErrorInvalidValue; launch_row8<1>(a, grid, s); break;
+            case 2: if (a.g.bpm != 4) return hipErrorInvalidValue; launch_row8<2>(a, grid, s); break;
+            case 4: if (a.g.bpm != 6) return hipErrorInvalidValue; launch_row8<4>(a, grid, s); break;
+            default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
-    if (a.solo) {
-        if (a.maxval == 255)
-            hipLaunchKernelGGL((fdct_kernel<true, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
-        else
-            hipLaunchKernelGGL((fdct_kernel<false, kK1WavesSolo>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
-    } else {
-        if (a.maxval == 255)
-            hipLaunchKernelGGL((fdct_kernel<true, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
-        else
-            hipLaunchKernelGGL((fdct_kernel<false, kK1WavesShared>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+    if (a.g.yh != 2 || a.g.bpm != 6) return hipErrorInvalidValue;
+    switch (a.g.cfilt) {
+        case kFiltS420m: launch_420<kFiltS420m>(a, grid, s); break;
+        case kFiltS420lm: launch_420<kFiltS420lm>(a, grid, s); break;
+        case kFiltS420: launch_420<kFiltS420>(a, grid, s); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

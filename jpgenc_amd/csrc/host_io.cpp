@@ -172,7 +172,7 @@ void quality_tables(int q, uint8_t qy[64], uint8_t qc[64]) {
 }
 
 std::vector<uint8_t> jfif_headers(uint32_t rw, uint32_t rh, const uint8_t qy[64], const uint8_t qc[64],
-                                  const HuffTable* const tables[4], uint32_t restart_mcus, bool s444) {
+                                  const HuffTable* const tables[4], uint32_t restart_mcus, uint8_t ysamp) {
     std::vector<uint8_t> o;
     o.reserve(700);
     // sSOI + sAPP0 (JpegSegments.hpp:55-109): JFIF 1.1, no units, density 1x1.
@@ -186,10 +186,11 @@ std::vector<uint8_t> jfif_headers(uint32_t rw, uint32_t rh, const uint8_t qy[64]
         for (int i = 0; i < 64; ++i) o.push_back(qt[id][kZigzagToNatural[i]]);
     }
     // sSOF0 (JpegSegments.hpp:112-164): height before width, unpadded size;
-    // Y 2x2 on table 0, Cb/Cr 1x1 on table 1 (Image.cpp:940-945); Y 1x1 at 4:4:4.
+    // Y 2x2 on table 0, Cb/Cr 1x1 on table 1 (Image.cpp:940-945); the other
+    // subsampling modes declare Y as ysamp = (H << 4) | V.
     o.push_back(0xFF); o.push_back(0xC0); put16(o, 17); o.push_back(8);
     put16(o, rh & 0xFFFF); put16(o, rw & 0xFFFF);
-    const uint8_t comp[10] = {3, 1, (uint8_t)(s444 ? 0x11 : 0x22), 0, 2, 0x11, 1, 3, 0x11, 1};
+    const uint8_t comp[10] = {3, 1, ysamp, 0, 2, 0x11, 1, 3, 0x11, 1};
     o.insert(o.end(), comp, comp + 10);
     // sDHT x4 (JpegSegments.hpp:167-256), Image.cpp:946-949.
     static const uint8_t kInfo[4] = {0x00, 0x10, 0x01, 0x11};

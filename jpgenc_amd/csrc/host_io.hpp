@@ -57,7 +57,7 @@ extern const uint8_t kZigzagToNatural[64];
 // segment before SOS, s444 declares Y 1x1 (both not in the reference).
 std::vector<uint8_t> jfif_headers(uint32_t real_width, uint32_t real_height, const uint8_t qy[64],
                                   const uint8_t qc[64], const HuffTable* const tables[4], uint32_t restart_mcus = 0,
-                                  bool s444 = false);
+                                  uint8_t ysamp = 0x22);
 
 // Deterministic synthetic RGB8 frame (integer-only, identical on every host):
 // kind 0 = smooth gradients + texture + noise (photo-like), 1 = uniform random

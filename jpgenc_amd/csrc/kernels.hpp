@@ -24,16 +24,24 @@ namespace jpge {
 
 // Frame geometry (reference: Image.cpp:480-531 pads to 16, Image.cpp:311-312
 // halves the chroma planes).  One MCU = 16x16 px = Y00 Y01 Y10 Y11 Cb Cr.
-// bpm = blocks per MCU: 6 at 4:2:0 (the reference's S420_m: 16x16 px MCUs of
-// Y00 Y01 Y10 Y11 Cb Cr), 3 at 4:4:4 (the S444 extension: 8x8 px MCUs of Y Cb Cr).
+// An MCU is yh x yv Y blocks (row by row) + one Cb + one Cr block, bpm = yh*yv + 2:
+//   4:2:0 (the reference's S420_m, and the S420 / S420_lm filters): 2x2, 16x16 px;
+//   4:4:4: 1x1, 8x8 px;  4:2:2: 2x1, 16x8 px;  4:1:1: 4x1, 32x8 px.
+// cfilt selects the 4:2:0 chroma filter of applySubsampling (Image.cpp:279-306).
+constexpr uint32_t kFiltS420m = 0, kFiltS420lm = 1, kFiltS420 = 2;
 struct Geometry {
     uint32_t width = 0, height = 0;  // real size
     uint32_t mw = 0, mh = 0;         // MCUs per row / column
     uint32_t bpm = 6;
+    uint32_t yh = 2;                 // Y blocks across an MCU (1, 2, 4)
+    uint32_t cfilt = kFiltS420m;
     JPGE_HD uint32_t nmcu() const { return mw * mh; }
     JPGE_HD uint32_t nblocks() const { return nmcu() * bpm; }
+    JPGE_HD uint32_t yv() const { return (bpm - 2) / yh; }  // Y blocks down an MCU (1, 2)
     JPGE_HD bool s444() const { return bpm == 3; }
-    JPGE_HD uint32_t mcu_px() const { return bpm == 3 ? 8u : 16u; }  // MCU edge in pixels
+    JPGE_HD bool row8() const { return bpm - 2 == yh; }  // MCUs one block row high
+    JPGE_HD uint32_t mcu_w() const { return 8 * yh; }   // MCU size in pixels
+    JPGE_HD uint32_t mcu_h() const { return 8 * yv(); }
 };
 // component of MCU slot k: 0 = Y, 1 = Cb, 2 = Cr (the last two slots are the chroma)
 JPGE_HD inline int block_comp(int k, uint32_t bpm) { return k < (int)bpm - 2 ? 0 : k - ((int)bpm - 3); }

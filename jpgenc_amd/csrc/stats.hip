@@ -43,9 +43,10 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     JPGE_STAMP(0);
     // key bases: Y raster index of the first Y block row of this workgroup's first
     // MCU row, chroma raster index of that MCU row (keys are relative to them)
-    const uint32_t bpm = a.g.bpm;  // 6 (4:2:0) or 3 (4:4:4: the Y text is in MCU order)
+    const uint32_t bpm = a.g.bpm, yh = a.g.yh, yv = a.g.yv();  // MCU = yh x yv Y blocks + Cb + Cr
+    const uint64_t ybw = (uint64_t)mw * yh;                    // Y blocks per block row
     const uint32_t mrow0 = (uint32_t)(((uint64_t)t_first * kK2Blocks) / bpm) / mw;
-    const uint64_t ybase = bpm == 3 ? (uint64_t)mrow0 * mw : 2ull * mrow0 * (2ull * mw);
+    const uint64_t ybase = (uint64_t)mrow0 * yv * ybw;
     const uint64_t cbase = (uint64_t)mrow0 * mw;
     const int lane = tid & 63, wv = tid >> 6;
     const int blk = block_of(wv, lane), part = part_of(wv);
@@ -72,12 +73,10 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         uint32_t rel;  // index of this block in its symbol text, relative to the bases
         int tsel;
         if (comp == 0) {
-            if (bpm == 3) {
-                rel = (uint32_t)(m6 - ybase);
-            } else {
-                const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
-                rel = (uint32_t)((2ull * mrow + (k >> 1)) * (2ull * mw) + 2ull * mcol + (k & 1) - ybase);
-            }
+            // raster index of Y slot k of MCU m6 (the Y text is in block raster order)
+            const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
+            rel = (uint32_t)(((uint64_t)mrow * yv + (uint32_t)k / yh) * ybw + (uint64_t)mcol * yh + (uint32_t)k % yh -
+                             ybase);
             tsel = 0;
         } else {
             rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);  // all Cr after all Cb

@@ -91,6 +91,6 @@ def test_s444_decodes(enc444):
 
 def test_s444_rejects_bad_mode_and_stripes(enc444):
     with pytest.raises(J.JpgeError):
-        enc444.set_subsampling(422)
+        enc444.set_subsampling(421)
     with pytest.raises(J.JpgeError):  # (rejected before the pointer is used)
         enc444.stripe_transform(16, 64 * 3, 64, 64, 0, 4)
