@@ -159,6 +159,37 @@ int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], ui
  * tools): writes n distinct symbols as (symbol, length, code) in DHT order. */
 int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t* codes, int* nsym);
 
+/* ---- Decode-side verification utilities (host) ---- */
+
+/* huffmanDecode (Huffman.hpp:62, Huffman.cpp:91-146): the symbol text coded in the
+ * first nbits bits (MSB-first bytes) by the table of nsym (symbol, code, length)
+ * entries, codes right-aligned as jpge_huffman_text returns them.  text = NULL:
+ * count only.  JPGE_E_FORMAT where no code matches (the reference asserts). */
+int jpge_huffman_decode(const uint8_t* bits, uint64_t nbits, const uint32_t* table_syms, const uint32_t* table_codes,
+                        const uint8_t* table_lens, int nsym, int* text, size_t cap, size_t* n);
+
+/* inverseDctMat (Dct.hpp:278-306) of one 8x8 block, row-major doubles:
+ * (A^T X) A with A(k, n) = C(k) sqrt(2/8) cos((2n+1) k pi / 16). */
+void jpge_idct8x8(const double in[64], double out[64]);
+
+/* A decoded jpge stream's frame (jpge_decode_coeffs). */
+typedef struct {
+    uint32_t width, height;  /* SOF0: the real size */
+    uint32_t yh, yv;         /* Y sampling factors (chroma is 1x1) */
+    uint32_t restart;        /* DRI interval in MCUs, 0 = none */
+    size_t y_blocks, c_blocks; /* coefficient blocks per plane */
+    uint8_t qy[64], qc[64];  /* DQT tables, natural order */
+} jpge_decoded;
+
+/* Baseline entropy decode of a .jpg written by this library (SOF0, three
+ * components, chroma 1x1, Y 1x1 / 2x1 / 4x1 / 2x2, optional DRI/RSTn): the
+ * quantised coefficients with the DC differences undone (Image.cpp:638-678
+ * inverted), natural order, blocks in raster order per component — the planes
+ * jpge_fdct_quant returns.  y = NULL: fill *info only (sizes).  Verification
+ * utility, not on the encode path. */
+int jpge_decode_coeffs(const uint8_t* jpg, size_t len, jpge_decoded* info, int16_t* y, int16_t* cb, int16_t* cr,
+                       size_t cap_y_blocks, size_t cap_c_blocks);
+
 /* PPM front end — replaces loadPPM (Image.hpp:28, Image.cpp:421-538) up to the
  * padding, which the GPU path performs by clamped addressing.  parse: rgb gets
  * width*height*3 unscaled samples (cap bytes available). */

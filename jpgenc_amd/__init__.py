@@ -39,6 +39,7 @@ EXPORTS = (
     "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_encode_files", "jpge_synth_rgb8", "jpge_arai_constants",
     "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
+    "jpge_huffman_decode", "jpge_idct8x8", "jpge_decode_coeffs",
 )
 
 
@@ -74,6 +75,13 @@ class StripeSummary(ctypes.Structure):
         for i in range(8):
             s.ff[i] = t[1][i]
         return s
+
+
+class Decoded(ctypes.Structure):
+    """jpge_decoded: the frame header of a decoded jpge stream."""
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("yh", ctypes.c_uint32),
+                ("yv", ctypes.c_uint32), ("restart", ctypes.c_uint32), ("y_blocks", ctypes.c_size_t),
+                ("c_blocks", ctypes.c_size_t), ("qy", ctypes.c_uint8 * 64), ("qc", ctypes.c_uint8 * 64)]
 
 
 class Timing(ctypes.Structure):
@@ -130,6 +138,10 @@ def lib() -> ctypes.CDLL:
         L.jpge_synth_rgb8.argtypes = [ctypes.c_uint64, u32, u32, i32, vp, sz]
         L.jpge_arai_constants.argtypes = [vp, vp]
         L.jpge_arai_constants.restype = None
+        L.jpge_huffman_decode.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, i32, vp, sz, ctypes.POINTER(sz)]
+        L.jpge_idct8x8.argtypes = [vp, vp]
+        L.jpge_idct8x8.restype = None
+        L.jpge_decode_coeffs.argtypes = [vp, sz, ctypes.POINTER(Decoded), vp, vp, vp, sz, sz]
         _LIB = L
     return _LIB
 
@@ -200,6 +212,44 @@ def huffman_text(text) -> list[tuple[int, int, int]]:
     k = ctypes.c_int()
     _check(lib().jpge_huffman_text(_p(t), t.size, _p(syms), _p(lens), _p(codes), ctypes.byref(k)), "huffman_text")
     return list(zip(syms[:k.value].tolist(), lens[:k.value].tolist(), codes[:k.value].tolist()))
+
+
+def huffman_decode(data: bytes, nbits: int, table) -> list[int]:
+    """huffmanDecode (Huffman.cpp:91-146): the symbols coded in the first nbits bits of
+    data by table = [(symbol, length, code)] (as huffman_text returns it)."""
+    buf = np.frombuffer(bytes(data) + b"\0", np.uint8)
+    syms = np.ascontiguousarray([t[0] for t in table], np.uint32)
+    lens = np.ascontiguousarray([t[1] for t in table], np.uint8)
+    codes = np.ascontiguousarray([t[2] for t in table], np.uint32)
+    n = ctypes.c_size_t()
+    _check(lib().jpge_huffman_decode(_p(buf), nbits, _p(syms), _p(codes), _p(lens), len(table), None, 0,
+                                     ctypes.byref(n)), "huffman_decode")
+    out = np.zeros(max(1, n.value), np.int32)
+    _check(lib().jpge_huffman_decode(_p(buf), nbits, _p(syms), _p(codes), _p(lens), len(table), _p(out), out.size,
+                                     ctypes.byref(n)), "huffman_decode")
+    return out[:n.value].tolist()
+
+
+def idct8x8(block) -> np.ndarray:
+    """inverseDctMat (Dct.hpp:278-306) of an 8x8 block."""
+    x = np.ascontiguousarray(block, np.float64).reshape(64)
+    out = np.zeros(64, np.float64)
+    lib().jpge_idct8x8(_p(x), _p(out))
+    return out.reshape(8, 8)
+
+
+def decode_coeffs(data: bytes):
+    """Entropy-decode a jpge .jpg -> (Decoded header, Y, Cb, Cr) quantised coefficient
+    planes of shape (blocks, 64), raster block order, natural order (jpge_decode_coeffs)."""
+    buf = np.frombuffer(bytes(data), np.uint8)
+    info = Decoded()
+    _check(lib().jpge_decode_coeffs(_p(buf), buf.size, ctypes.byref(info), None, None, None, 0, 0), "decode_coeffs")
+    y = np.zeros((info.y_blocks, 64), np.int16)
+    cb = np.zeros((info.c_blocks, 64), np.int16)
+    cr = np.zeros_like(cb)
+    _check(lib().jpge_decode_coeffs(_p(buf), buf.size, ctypes.byref(info), _p(y), _p(cb), _p(cr), y.shape[0],
+                                    cb.shape[0]), "decode_coeffs")
+    return info, y, cb, cr
 
 
 def huffman_table(counts, first):

@@ -68,4 +68,21 @@ int64_t ref_pack_bits(const uint32_t* vals, const int* nbits, const int* modes, 
     return (int64_t)b.size();
 }
 
+// The reference's own round trip (HuffmanTest.cpp:65-85): generateHuffmanCode,
+// huffmanEncode (Huffman.cpp:69-76) and huffmanDecode (Huffman.cpp:91-146).  bits
+// receives the encoded stream MSB-first (cap bytes, zeroed by the caller); decoded
+// the decoded text (n entries).  Returns the bit count.
+int64_t ref_huffman_roundtrip(const int* text, int n, uint8_t* bits, int64_t cap, int* decoded) {
+    std::vector<int> t(text, text + n);
+    auto res = generateHuffmanCode(t);
+    Bitstream enc = huffmanEncode(t, res.first);
+    const int64_t nb = (int64_t)enc.size();
+    if ((nb + 7) / 8 > cap) return -1;
+    for (int64_t i = 0; i < nb; ++i)
+        if (enc.extract(1, (unsigned)i) >> 31) bits[i >> 3] |= (uint8_t)(0x80u >> (i & 7));
+    std::vector<int> dec = huffmanDecode(enc, res.first);
+    for (size_t i = 0; i < dec.size() && i < (size_t)n; ++i) decoded[i] = dec[i];
+    return nb;
+}
+
 }  // extern "C"
