@@ -45,6 +45,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     // MCU row, chroma raster index of that MCU row (keys are relative to them)
     const uint32_t bpm = a.g.bpm, yh = a.g.yh, yv = a.g.yv();  // MCU = yh x yv Y blocks + Cb + Cr
     const uint64_t ybw = (uint64_t)mw * yh;                    // Y blocks per block row
+    const uint32_t yhs = (uint32_t)__builtin_ctz(yh);          // yh is 1, 2 or 4: k / yh = k >> yhs
     const uint32_t mrow0 = (uint32_t)(((uint64_t)t_first * kK2Blocks) / bpm) / mw;
     const uint64_t ybase = (uint64_t)mrow0 * yv * ybw;
     const uint64_t cbase = (uint64_t)mrow0 * mw;
@@ -75,8 +76,8 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         if (comp == 0) {
             // raster index of Y slot k of MCU m6 (the Y text is in block raster order)
             const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
-            rel = (uint32_t)(((uint64_t)mrow * yv + (uint32_t)k / yh) * ybw + (uint64_t)mcol * yh + (uint32_t)k % yh -
-                             ybase);
+            rel = (uint32_t)(((uint64_t)mrow * yv + ((uint32_t)k >> yhs)) * ybw + (uint64_t)mcol * yh +
+                             ((uint32_t)k & (yh - 1)) - ybase);
             tsel = 0;
         } else {
             rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);  // all Cr after all Cb
