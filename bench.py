@@ -38,6 +38,10 @@ W4K, H4K = 3840, 2160
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+# subsampling modes (jpge.h JPGE_S*) -> the name in the metric / workload
+SUB_NAMES = {420: "4:2:0", 444: "4:4:4", 422: "4:2:2", 411: "4:1:1", 4200: "4:2:0 S420", 4201: "4:2:0 S420_lm"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -58,8 +62,9 @@ def parse():
     ap.add_argument("--restart", type=int, default=None,
                     help="restart interval in MCUs (16k-striped: default 1024 = one interval per MCU row, "
                          "the config's 'tiled with restart intervals'; 0 = the reference's single interval)")
-    ap.add_argument("--subsampling", type=int, choices=[420, 444], default=420,
-                    help="4k-frames: chroma subsampling (420 = the reference's S420_m; 444 = the S444 extension)")
+    ap.add_argument("--subsampling", type=int, choices=sorted(SUB_NAMES), default=420,
+                    help="4k-frames: subsampling mode (jpge.h JPGE_S*: 420 = the reference's S420_m; "
+                         "444, 422, 411, 4200 = S420, 4201 = S420_lm are extensions)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
@@ -140,7 +145,7 @@ def cpu_baseline(args) -> dict:
 
 
 def sub_name(args) -> str:
-    return "4:4:4" if getattr(args, "subsampling", 420) == 444 else "4:2:0"
+    return SUB_NAMES[getattr(args, "subsampling", 420)]
 
 
 def cgroup_cpu_stat() -> dict:
@@ -404,7 +409,8 @@ def main():
     npx = W * H
     avg_jpeg = total_bytes / (args.steps * F)
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H) if args.subsampling == 420 else {}
-    cb = 6.0 if args.subsampling == 444 else 3.0  # coefficient bytes per pixel (3 or 1.5 int16)
+    yh, yv = J.SUBSAMPLING[args.subsampling]
+    cb = 2.0 * 64 * (yh * yv + 2) / (64 * yh * yv)  # int16 coefficient bytes per pixel (4:2:0: 3)
     alg = {
         "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
         "stats_kernel": (cb * npx, f"coefficients read {cb:g} B/px"),
