@@ -6,7 +6,7 @@
 // 16 zig-zag positions of 64 blocks.  Persistent grid:
 // each workgroup owns a contiguous run of 128-block tiles (the next one is loaded
 // into registers while the current one is counted), accumulates into LDS
-// (8 copies of the AC counters cap same-address atomics at 8 lanes) and flushes
+// (8 bank-staggered copies of the AC counters cap same-address atomics at 8 lanes) and flushes
 // once into kHistReplicas global replicas.  First-occurrence keys (text index of
 // the symbol, see huffman.hpp) are kept workgroup-relative in u32 LDS words and
 // widened at the flush; the global key is stored inverted so atomicMax keeps the
@@ -20,10 +20,16 @@ using namespace dev;
 constexpr int kK2Blocks = kStatsTile;
 constexpr int kK2Threads = kK2Blocks * kPartsPerBlock;
 constexpr int kHistCopies = 8;
+// Copy stride 512 + 4 words: LDS atomics bank by (word mod 32), so an unpadded
+// stride (512) put every copy of a symbol on one bank and the copies only turned
+// same-address serialisation into same-bank conflicts.  With +4 the 8 copies of a
+// symbol sit on banks s, s+4, ..., s+28 (bank-conflict cycles halved; 16 copies at
+// +2 removed only 7% more and cost LDS occupancy in the pipeline).
+constexpr int kCopyWords = 2 * 256 + 4;
 
 struct K2Lds {
     int16_t zz[kK2Blocks * kZzStride];
-    uint32_t acnt[kHistCopies][2][256];  // AC counters (Y-AC, C-AC), per copy
+    uint32_t acnt[kHistCopies][kCopyWords];  // AC counters (Y-AC at 0, C-AC at 256), per copy
     uint32_t dcnt[2][16];                // DC counters (Y-DC, C-DC)
     uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
     uint64_t bmask[kK2Blocks];
@@ -37,7 +43,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     const uint32_t ntiles = (nblocks + kK2Blocks - 1) / kK2Blocks;
     const uint32_t t_first = (uint32_t)((uint64_t)blockIdx.x * ntiles / gridDim.x);
     const uint32_t t_last = (uint32_t)((uint64_t)(blockIdx.x + 1) * ntiles / gridDim.x);
-    for (int i = tid; i < kHistCopies * 512; i += kK2Threads) (&lds.acnt[0][0][0])[i] = 0;
+    for (int i = tid; i < kHistCopies * kCopyWords; i += kK2Threads) (&lds.acnt[0][0])[i] = 0;
     for (int i = tid; i < 1024; i += kK2Threads) (&lds.key[0][0])[i] = 0xFFFFFFFFu;
     if (tid < 32) (&lds.dcnt[0][0])[tid] = 0;
     JPGE_STAMP(0);
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
             if (rel < *kp) atomicMin(kp, rel);
         }
         const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
-        uint32_t* cnt = lds.acnt[lane & (kHistCopies - 1)][tsel];
+        uint32_t* cnt = &lds.acnt[lane & (kHistCopies - 1)][tsel * 256];
         uint32_t* key = lds.key[2 * tsel + 1];
         for_each_ac(pv, part, [&](int p, int run, int v) {
             const int sym = ((run & 15) << 4) | category(v);
@@ -123,7 +129,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         const bool ac = t & 1;
         uint32_t c = 0;
         if (ac) {
-            for (int cp = 0; cp < kHistCopies; ++cp) c += lds.acnt[cp][t >> 1][s];
+            for (int cp = 0; cp < kHistCopies; ++cp) c += lds.acnt[cp][(t >> 1) * 256 + s];
         } else if (s < 16) {
             c = lds.dcnt[t >> 1][s];
         }
