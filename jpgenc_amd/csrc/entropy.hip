@@ -34,6 +34,7 @@ constexpr int kMaxTiles = kEntropyMaxTilesPerWg;
 constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-case tile + lead
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
+static_assert(kWinWords == 8 && kEntropyRegionBytes % 16 == 0, "pack loads a window as two aligned uint4");
 constexpr int kChunk = kK3Threads * kWin;                             // output bytes per round (pre-stuffing)
 // One part's bits: DC <= 16+11, 16 AC symbols <= 16+11 each, <= 3 ZRL (a part
 // spans 16 positions, so only its first run can reach 16), EOB <= 16 -> < 512.
@@ -591,10 +592,17 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
         uint32_t y[kWinWords];
         uint32_t cff = 0;
         if (j0 < jhi) {
-            uint32_t prev = rword((int64_t)(j0 / 4) - 1);
+            // the window's 8 words as two 16-byte loads (j0 is a multiple of 32 and the
+            // region keeps 128 bytes of slack past its worst case, so they stay inside
+            // it; words at or past nwr are masked to 0 as rword does)
+            const uint32_t w0 = j0 / 4;
+            const uint4* R4 = reinterpret_cast<const uint4*>(R32 + w0);
+            const uint4 lo = R4[0], hi = R4[1];
+            const uint32_t raw[kWinWords] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            uint32_t prev = rword((int64_t)w0 - 1);
 #pragma unroll
             for (int m = 0; m < kWinWords; ++m) {  // output word = R shifted right by b bits
-                const uint32_t cur = rword((int64_t)(j0 / 4) + m);
+                const uint32_t cur = w0 + m < nwr ? __builtin_bswap32(raw[m]) : 0u;
                 y[m] = __builtin_amdgcn_alignbit(prev, cur, b);
                 prev = cur;
             }
