@@ -26,11 +26,14 @@ constexpr int kHistCopies = 8;
 // symbol sit on banks s, s+4, ..., s+28 (bank-conflict cycles halved; 16 copies at
 // +2 removed only 7% more and cost LDS occupancy in the pipeline).
 constexpr int kCopyWords = 2 * 256 + 4;
+// DC counters: one wave's 64 lanes count a handful of categories; the same copies
+// and bank stagger (stride 36 words) split them.
+constexpr int kDcCopyWords = 2 * 16 + 4;
 
 struct K2Lds {
     int16_t zz[kK2Blocks * kZzStride];
     uint32_t acnt[kHistCopies][kCopyWords];  // AC counters (Y-AC at 0, C-AC at 256), per copy
-    uint32_t dcnt[2][16];                // DC counters (Y-DC, C-DC)
+    uint32_t dcnt[kHistCopies][kDcCopyWords];  // DC counters (Y-DC at 0, C-DC at 16), per copy
     uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
     uint64_t bmask[kK2Blocks];
     int prevdc[6];
@@ -45,7 +48,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     const uint32_t t_last = (uint32_t)((uint64_t)(blockIdx.x + 1) * ntiles / gridDim.x);
     for (int i = tid; i < kHistCopies * kCopyWords; i += kK2Threads) (&lds.acnt[0][0])[i] = 0;
     for (int i = tid; i < 1024; i += kK2Threads) (&lds.key[0][0])[i] = 0xFFFFFFFFu;
-    if (tid < 32) (&lds.dcnt[0][0])[tid] = 0;
+    for (int i = tid; i < kHistCopies * kDcCopyWords; i += kK2Threads) (&lds.dcnt[0][0])[i] = 0;
     JPGE_STAMP(0);
     // key bases: Y raster index of the first Y block row of this workgroup's first
     // MCU row, chroma raster index of that MCU row (keys are relative to them)
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         pv.load(lds.zz, mask, blk, part, active);
         if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
             const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst, bpm));
-            atomicAdd(&lds.dcnt[tsel][dcat], 1u);
+            atomicAdd(&lds.dcnt[lane & (kHistCopies - 1)][tsel * 16 + dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
         }
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         if (ac) {
             for (int cp = 0; cp < kHistCopies; ++cp) c += lds.acnt[cp][(t >> 1) * 256 + s];
         } else if (s < 16) {
-            c = lds.dcnt[t >> 1][s];
+            for (int cp = 0; cp < kHistCopies; ++cp) c += lds.dcnt[cp][(t >> 1) * 16 + s];
         }
         if (!c) continue;
         atomicAdd(&a.hist.cnt[(rep * 4 + t) * 256 + s], c);
