@@ -1,29 +1,42 @@
 """jpge benchmark — BASELINE.json metric: MPixels/s encode (4K 4:2:0 Q=90).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--quality Q]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 4k-frames|batch1080|16k-striped|ppm-files]
 
-A step = one pass of the full encode path (RGB8 in HBM -> finished .jpg bytes in
-HBM: colour/4:2:0/FDCT/quantise + statistics kernels, host Huffman-table build,
-entropy+stuffing kernel) over a batch of F distinct synthetic 3840x2160 frames
-resident in HBM (F=16 by default: 16 x 24.9 MB > the 256 MB Infinity Cache, so
-the colour/DCT stage reads from HBM).  Frames are independent, so with N GPUs
-each rank encodes its own F frames (weak scaling, no data-path collective);
-the gloo process group only provides the barriers and the max-over-ranks time.
+Launch: `--gpus N` under torch.distributed.run uses its RANK/WORLD_SIZE; without a
+launcher (WORLD_SIZE unset) and N > 1 this script starts the N rank processes
+itself, before anything touches a GPU, and exits with the worst rank's status.
+Only rank 0 prints.
 
-Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel (largest
-HIP-event time per frame on its own stream inside the timed region); `stages`
-carries all three kernels, each with its algorithmic bytes per launch:
-  fdct_kernel    RGB8 read 3 B/px + int16 coefficients written 3 B/px
-  stats_kernel   coefficients read 3 B/px
-  entropy_kernel coefficients read 3 B/px + entropy-coded bytes written
-`traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary
-(profiles/pmc_r01.json, FETCH_SIZE doubled on gfx950).  The CPU baseline is the
-test-only oracle on the host cores, rank 0 at N=1.
+Workloads (a step = one pass of the full encode path over a batch of synthetic
+frames resident in HBM: colour/4:2:0/FDCT/quantise + statistics kernels, host
+Huffman-table build, entropy code + pack kernels, finished .jpg bytes in HBM):
+  4k-frames  (default; BASELINE metric, SURVEY 8(e) frames): F = 768 frames of
+             3840x2160 Q90 per GPU per step, cycling over D = 32 distinct inputs
+             (800 MB > the 256 MB Infinity Cache, so K1 reads from HBM); frames are
+             independent, each rank encodes its own (weak scaling, no data-path
+             collective; the gloo group only carries barriers and the max time).
+  batch1080  (config 4): one batch of 256 distinct 1920x1080 Q90 frames (seeds
+             1000+i) per step, dealt over the ranks (frame i -> rank i mod N:
+             strong scaling); the .jpg segments are gathered to rank 0 over RCCL
+             (grouped send/recv) inside the step.
+  16k-striped (config 5): one 16384^2 frame per step, row-striped over the ranks.
+  ppm-files  (SURVEY 8(f) rank 1): PPM files -> .jpg files (PCIe-inclusive).
+
+The 4k-frames line carries: `roofline` = the dominant kernel in situ (HIP events on
+its lane's stream inside the timed region), `roofline_dct_stage` = K1 alone (the
+BASELINE figure, with its HBM-read-only fraction), `roofline_pipeline`, per-stage
+rooflines (algorithmic bytes per launch), `verified` (every output of
+the last timed step byte-compared with the host-path encode of its frame, and a
+sample with the CPU oracle), `d2h` (device RGB -> .jpg bytes in pinned host
+memory, SURVEY 8(d)'s end-to-end definition) and `cpu_baseline` (the test-only
+oracle on the host cores, rank 0 at N=1; the reference's own figure from this
+container's BASELINE.md beside it).
 """
 from __future__ import annotations
 
 import argparse
 import collections
+import hashlib
 import json
 import os
 import sys
@@ -36,29 +49,41 @@ sys.path.insert(0, ROOT)
 
 W4K, H4K = 3840, 2160
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# The reference's own encoder (writeJPEG) at 4K 4:2:0 Q90, timed in the survey
+# container (1874 ms on 8 vCPU = 4.4 MPix/s); the reference needs
+# Boost, absent here and on the GPU box, so it cannot be rebuilt beside the GPU.
+REF_CPU_4K_Q90 = {"value": 4.4, "unit": "MPix/s", "cores": 8, "kind": "reference",
+                  "source": "BASELINE.md §2 (reference writeJPEG, 3840x2160 Q90, 8 vCPU Xeon, survey container)"}
 
 
 # subsampling modes (jpge.h JPGE_S*) -> the name in the metric / workload
 SUB_NAMES = {420: "4:2:0", 444: "4:4:4", 422: "4:2:2", 411: "4:1:1", 4200: "4:2:0 S420", 4201: "4:2:0 S420_lm"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per GPU per step (4k-frames: 768; batch1080: the whole batch, 256)")
+    ap.add_argument("--distinct", type=int, default=32, help="4k-frames: distinct input frames the step cycles over")
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--width", type=int, default=W4K)
     ap.add_argument("--height", type=int, default=H4K)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-timing output verification")
+    ap.add_argument("--d2h-steps", type=int, default=5, help="steps of the D2H-inclusive pass (0 = skip)")
     ap.add_argument("--solo-batches", type=int, default=2,
                     help="batches through a 1-lane encoder after the timed region (kernel times alone; 0 = skip)")
     ap.add_argument("--lanes", type=int, default=0, help="encoder lanes (0 = library default)")
-    ap.add_argument("--workload", choices=["4k-frames", "16k-striped", "ppm-files"], default="4k-frames",
-                    help="4k-frames: the BASELINE metric (frames sharded over ranks); 16k-striped: one "
-                         "16384x16384 frame per step, row-striped over the ranks (SURVEY 8(e) config 5); "
-                         "ppm-files: PPM files -> .jpg files through the ingest pipeline (PCIe-inclusive)")
+    ap.add_argument("--workload", choices=["4k-frames", "batch1080", "16k-striped", "ppm-files", "dist-check"],
+                    default="4k-frames",
+                    help="4k-frames: the BASELINE metric (frames sharded over ranks); batch1080: config 4 (256 "
+                         "1080p frames per step dealt over the ranks, segments gathered to rank 0); 16k-striped: "
+                         "one 16384x16384 frame per step, row-striped over the ranks (config 5); ppm-files: PPM "
+                         "files -> .jpg files through the ingest pipeline (PCIe-inclusive); dist-check: the "
+                         "launcher and reductions only, no GPU (CPU tests)")
     ap.add_argument("--restart", type=int, default=None,
                     help="restart interval in MCUs (16k-striped: default 1024 = one interval per MCU row, "
                          "the config's 'tiled with restart intervals'; 0 = the reference's single interval)")
@@ -69,13 +94,53 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
                     help="bracket the kernels of every N-th frame with HIP events (each event costs GPU time)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------- launch / ranks
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn(n: int, argv: list[str]) -> int:
+    """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* as
+    torch.distributed.run sets them) and wait for them.  Called before anything
+    touches a GPU.  A rank that fails ends the others; returns the worst status."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:  # (our own children, by handle)
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def dist_setup(n_gpus: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and n_gpus > 1 and n_gpus != world:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
     pg = None
     if world > 1:
         import torch.distributed as dist
@@ -111,13 +176,42 @@ def sum_over_ranks(pg, v: float) -> float:
     return float(t.item())
 
 
+def device_for(local: int) -> int:
+    """This rank's GPU: LOCAL_RANK, wrapped when the box has fewer GPUs than ranks (a
+    rehearsal of N ranks on one GPU; the driver's N-GPU runs have one GPU per rank)."""
+    import torch
+
+    return local % max(1, torch.cuda.device_count())
+
+
+def gather_group(world: int):
+    """Process group for the data-path collectives: RCCL ("nccl") when every rank
+    has its own GPU, else gloo (ranks sharing a GPU; tensors staged through the host)."""
+    import torch
+    import torch.distributed as dist
+
+    return dist.new_group(backend="nccl" if torch.cuda.device_count() >= world else "gloo")
+
+
 def frame_seed(rank: int, i: int) -> int:
     return 3 + 1000 * rank + i  # config 3 seed family (SURVEY 8d), distinct per rank and frame
 
 
-def cpu_baseline(args) -> dict:
+def batch_seed(i: int) -> int:
+    return 1000 + i  # config 4: 256 x 1080p, seeds 1000+i (SURVEY 8d)
+
+
+def batch_share(total: int, rank: int, world: int) -> list[int]:
+    """Frames of a config-4 batch that `rank` encodes (frame i -> rank i mod world)."""
+    return list(range(rank, total, world))
+
+
+# ---------------------------------------------------------------- CPU baseline
+
+def cpu_baseline(args) -> tuple[dict, dict]:
     """The test-only oracle (CPU restatement of the reference path) on a bounded
-    sample of the same workload: whole 4K Q90 frames until ~cpu_seconds."""
+    sample of the same workload: whole 4K Q90 frames until ~cpu_seconds.  Also
+    returns {frame index: sha256 of the oracle's bytes} for the output check."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle  # noqa: E402
     import jpgenc_amd as J
@@ -125,11 +219,13 @@ def cpu_baseline(args) -> dict:
     threads = min(16, os.cpu_count() or 1)
     _oracle.orc().orc_set_threads(threads)
     enc_times = []  # encode-only time per frame (synthesis excluded)
+    hashes = {}
     for i in range(16):
         rgb = J.synth_rgb8(frame_seed(0, i), args.width, args.height)
         s = time.perf_counter()
-        _oracle.encode(rgb, args.quality, subsampling=args.subsampling)
+        out = _oracle.encode(rgb, args.quality, subsampling=args.subsampling)
         enc_times.append(time.perf_counter() - s)
+        hashes[i] = hashlib.sha256(out).hexdigest()
         if sum(enc_times) >= args.cpu_seconds:
             break
     px = args.width * args.height * len(enc_times)
@@ -141,7 +237,9 @@ def cpu_baseline(args) -> dict:
         "sample": f"{len(enc_times)} x {args.width}x{args.height} {sub_name(args)} Q{args.quality} frames (seeds 3..), "
                   f"oracle/jpge_oracle.cpp restatement, OpenMP {threads} threads (DCT/quant parallel, "
                   f"like the reference)",
-    }
+        "reference": REF_CPU_4K_Q90 if (args.width, args.height, args.quality, args.subsampling) ==
+        (W4K, H4K, 90, 420) else None,
+    }, hashes
 
 
 def sub_name(args) -> str:
@@ -174,21 +272,47 @@ def thread_cpu() -> dict:
 
 
 def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
-    """Per-launch HBM bytes per stage from the committed rocprofv3 PMC summary (the
-    entropy stage = its code, placement-scan and pack kernels)."""
+    """Per-launch HBM bytes per stage from the newest committed rocprofv3 PMC summary
+    (profiles/pmc_rNN.json; the entropy stage = its code, placement-scan and pack kernels)."""
     try:
-        with open(os.path.join(profile_dir, "pmc_r01.json")) as f:
+        names = sorted(f for f in os.listdir(profile_dir) if f.startswith("pmc_r") and f.endswith(".json"))
+        with open(os.path.join(profile_dir, names[-1])) as f:
             d = json.load(f)
         if d.get("width") != width or d.get("height") != height:
             return {}
         per = {k.split("<")[0]: v["hbm_bytes_per_launch"] for k, v in d["kernels"].items()}
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError, KeyError, IndexError):
         return {}
     out = {k: v for k, v in per.items() if not k.startswith("entropy_")}
     ent = [v for k, v in per.items() if k.startswith("entropy_")]
     if ent:
         out["entropy_kernel"] = sum(ent)
     return out
+
+
+def host_cpu_use(cg0: dict, cg1: dict, dt: float):
+    if not cg0:
+        return None
+    return {"cpus_used": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e6 / dt, 2),
+            "throttled_periods": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
+            "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3, 1)}
+
+
+# ---------------------------------------------------------------- workloads
+
+def run_dist_check(args, rank, local, world, pg):
+    """The launcher and the reductions without a GPU (CPU tests of --gpus N;
+    JPGE_BENCH_FAIL_RANK=r makes rank r fail before the first barrier)."""
+    if os.environ.get("JPGE_BENCH_FAIL_RANK") == str(rank):
+        raise SystemExit(3)
+    barrier(pg)
+    dt = max_over_ranks(pg, 0.001 * (rank + 1))
+    n = sum_over_ranks(pg, 1.0)
+    share = batch_share(256, rank, world)
+    frames = sum_over_ranks(pg, float(len(share)))
+    if rank == 0:
+        print(json.dumps({"metric": "dist-check", "value": n, "unit": "ranks", "n_gpus": world, "max_time": dt,
+                          "batch_frames": frames, "rank0_first": share[:3]}), flush=True)
 
 
 def run_striped16k(args, rank, local, world, pg):
@@ -200,6 +324,7 @@ def run_striped16k(args, rank, local, world, pg):
     import jpgenc_amd as J
     from jpgenc_amd import stripes
 
+    local = device_for(local)
     torch.cuda.set_device(local)
     W = H = 16384
     restart = 1024 if args.restart is None else args.restart
@@ -218,7 +343,7 @@ def run_striped16k(args, rank, local, world, pg):
     else:
         import torch.distributed as dist
 
-        rccl = dist.new_group(backend="nccl")  # the exchanges and the gather ride RCCL over xGMI
+        rccl = gather_group(world)  # the exchanges and the gather ride RCCL over xGMI
         r0, nr = stripes.stripe_rows(H // 16, world, stripes.restart_align(W, restart))[rank]
         src = torch.from_numpy(np.ascontiguousarray(rgb[16 * r0:16 * (r0 + nr)]).reshape(-1)).to(f"cuda:{local}")
         del rgb
@@ -268,8 +393,9 @@ def run_ppm_files(args, rank, local, world, pg):
 
     import jpgenc_amd as J
 
+    local = device_for(local)
     torch.cuda.set_device(local)
-    W, H, F = args.width, args.height, args.frames
+    W, H, F = args.width, args.height, args.frames or 16
     tmp = tempfile.mkdtemp(prefix=f"jpge_ppm_{rank}_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
     try:
         ins, outs = [], []
@@ -309,45 +435,146 @@ def run_ppm_files(args, rank, local, world, pg):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def main():
-    args = parse()
-    rank, local, world, pg = dist_setup(args.gpus)
-    if args.workload == "ppm-files":
-        run_ppm_files(args, rank, local, world, pg)
-        if pg is not None:
-            pg.destroy_process_group()
-        return
-    if args.workload == "16k-striped":
-        run_striped16k(args, rank, local, world, pg)
-        if pg is not None:
-            pg.destroy_process_group()
-        return
+def out_capacity(J, w: int, h: int) -> int:
+    """Device output bytes per frame slot: half the RGB size (a Q90 4K frame codes to
+    ~3 MB of 24.9 MB) within the library's worst-case bound; a frame that does not fit
+    fails with JPGE_E_NOSPACE (the pack kernel checks the capacity)."""
+    return min(J.max_jpeg_bytes(w, h), (w * h * 3 // 2 + 4095) // 4096 * 4096)
+
+
+def run_batch1080(args, rank, local, world, pg):
+    """Config 4: a batch of B (256) distinct 1920x1080 Q90 frames per step, frame i
+    encoded by rank i mod N; every rank's .jpg segments are gathered to rank 0 over
+    RCCL (one grouped send/recv round) inside the step, so after each step rank 0
+    holds the whole batch's files.  Strong scaling (the batch is fixed)."""
     import torch
 
     import jpgenc_amd as J
 
+    local = device_for(local)
     torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+    W, H, B = 1920, 1080, args.frames or 256
+    share = batch_share(B, rank, world)
+    cap = out_capacity(J, W, H)
+    host = {i: J.synth_rgb8(batch_seed(i), W, H) for i in share}
+    ins = {i: torch.from_numpy(host[i].reshape(-1)).to(dev) for i in share}
+    outbuf = torch.empty(len(share) * cap, dtype=torch.uint8, device=dev)
+    frames = [(ins[i].data_ptr(), W, H, W * 3) for i in share]
+    outd = [(outbuf.data_ptr() + k * cap, cap) for k in range(len(share))]
+    enc = J.Encoder(local, lanes=args.lanes)
+    rccl = None
+    if world > 1:
+        import torch.distributed as dist
+
+        rccl = gather_group(world)
+        xdev = dev if dist.get_backend(rccl) == "nccl" else "cpu"  # (gloo: ranks sharing one GPU)
+        nmax = len(batch_share(B, 0, world))
+        lens_all = [torch.zeros(nmax, dtype=torch.int64, device=xdev) for _ in range(world)]
+        gather = torch.empty(B * cap if rank == 0 else 1, dtype=torch.uint8, device=xdev)
+
+    def step():
+        lens = enc.encode_batch_dev(frames, outd, quality=args.quality)
+        if rccl is None:
+            return lens
+        import torch.distributed as dist
+
+        mine = torch.zeros(nmax, dtype=torch.int64, device=xdev)
+        mine[:len(lens)] = torch.tensor(lens, dtype=torch.int64)
+        dist.all_gather(lens_all, mine, group=rccl)
+        src = outbuf if xdev == dev else outbuf.cpu()
+        ops = []
+        if rank == 0:
+            table = torch.stack(lens_all).cpu().tolist()
+            for r in range(1, world):
+                for k, i in enumerate(batch_share(B, r, world)):
+                    n = int(table[r][k])
+                    ops.append(dist.P2POp(dist.irecv, gather[i * cap:i * cap + n], dist.get_global_rank(rccl, r),
+                                          group=rccl))
+        else:
+            for k, n in enumerate(lens):
+                ops.append(dist.P2POp(dist.isend, src[k * cap:k * cap + n], dist.get_global_rank(rccl, 0),
+                                      group=rccl))
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+        return lens
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(pg)
+    cg0 = cgroup_cpu_stat()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lens = step()
+    torch.cuda.synchronize()
+    barrier(pg)
+    dt = time.perf_counter() - t0
+    cg1 = cgroup_cpu_stat()
+    dt_max = max_over_ranks(pg, dt)
+    nbytes = sum_over_ranks(pg, float(sum(lens)))
+    # verification: every frame of the last step, as rank 0 holds it, equals the
+    # host-path encode of that frame (rank 0's own frames are in its output slots)
+    bad = 0
+    if not args.no_verify:
+        if rank == 0:
+            for i in range(B):
+                ref = enc.encode(host[i] if i in host else J.synth_rgb8(batch_seed(i), W, H), quality=args.quality)
+                if i in host:
+                    k = share.index(i)
+                    got = outbuf[k * cap:k * cap + lens[k]]
+                else:
+                    got = gather[i * cap:i * cap + len(ref)].to(dev)
+                if not torch.equal(got, torch.frombuffer(bytearray(ref), dtype=torch.uint8).to(dev)):
+                    bad += 1
+        bad = int(sum_over_ranks(pg, float(bad)))
+    if rank == 0:
+        line = {
+            "metric": "MPixels/s encode (batch of 256 x 1920x1080 4:2:0 Q=90)",
+            "value": round(W * H * B * args.steps / dt_max / 1e6, 1), "unit": "MPix/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (deterministic splitmix64 photo-like frames, seeds 1000+i, HBM-resident)",
+            "config": {"workload": f"config 4: {B} x {W}x{H} 4:2:0 Q{args.quality} per step, frame i on rank i mod "
+                                   f"{world}" + (", .jpg segments gathered to rank 0 over RCCL (grouped send/recv)"
+                                                 if world > 1 else ""),
+                       "batch": B, "width": W, "height": H, "quality": args.quality,
+                       "avg_jpeg_bytes": int(nbytes / B), "parallelism": f"frames dealt over {world} GPU(s)"},
+            "verified": None if args.no_verify else {
+                "frames": B, "mismatches": bad,
+                "method": "every frame of the last step, as gathered on rank 0, byte-compared with the host-path "
+                          "encode of the same frame"},
+            "host_cpu": host_cpu_use(cg0, cg1, dt),
+        }
+        print(json.dumps(line), flush=True)
+    enc.close()
+    if bad:
+        raise SystemExit(f"batch1080: {bad} frames differ from the host-path encode")
+
+
+def run_frames(args, rank, local, world, pg):
+    """The BASELINE metric: 4K frames, F per GPU per step over D distinct inputs."""
+    import torch
+
+    import jpgenc_amd as J
+
+    local = device_for(local)
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
     enc = J.Encoder(local, lanes=args.lanes)
     enc.set_subsampling(args.subsampling)
-    W, H, F = args.width, args.height, args.frames
+    W, H = args.width, args.height
+    F = args.frames or 768
+    D = max(1, min(args.distinct, F))
     pitch = W * 3
-    cap = J.max_jpeg_bytes(W, H)
-    # HBM-resident input ring and output buffers (torch = device-memory plumbing)
-    ins = []
-    for i in range(F):
-        host = J.synth_rgb8(frame_seed(rank, i), W, H)
-        ins.append(torch.from_numpy(host.reshape(-1)).to(f"cuda:{local}"))
-    outs = [torch.empty(cap, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(F)]
+    cap = out_capacity(J, W, H)
+    # HBM-resident input ring and output slots (torch = device-memory plumbing)
+    host = [J.synth_rgb8(frame_seed(rank, i), W, H) for i in range(D)]
+    ins = [torch.from_numpy(h.reshape(-1)).to(dev) for h in host]
+    outbuf = torch.empty(F * cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    frames = [(t.data_ptr(), W, H, pitch) for t in ins]
-    outd = [(o.data_ptr(), cap) for o in outs]
-
-    # correctness guard on the timed configuration: the first frame must match the
-    # host-path encode (which the parity tests pin to the oracle)
-    lens = enc.encode_batch_dev(frames[:1], outd[:1], quality=args.quality)
-    dev_bytes = outs[0][: lens[0]].cpu().numpy().tobytes()
-    if dev_bytes != enc.encode(J.synth_rgb8(frame_seed(rank, 0), W, H), quality=args.quality):
-        raise RuntimeError("device-resident path differs from the host path")
+    frames = [(ins[i % D].data_ptr(), W, H, pitch) for i in range(F)]
+    outd = [(outbuf.data_ptr() + i * cap, cap) for i in range(F)]
 
     for _ in range(args.warmup):
         enc.encode_batch_dev(frames, outd, quality=args.quality)
@@ -387,20 +614,60 @@ def main():
     pixels = sum_over_ranks(pg, float(W * H * F * args.steps))
     value = pixels / dt_max / 1e6
 
-    # Solo pass (after the timed region, not part of `value`): the same frames through
-    # a single-lane encoder with events around every frame's kernels, so each kernel's
-    # duration is its own, without other lanes' kernels beside it.
+    # Verification (after timing): every output slot of the last timed step equals
+    # the host-path encode of its input frame (byte compare on the device).
+    verified = None
+    refs = {}
+    if not args.no_verify:
+        for d in range(D):
+            refs[d] = enc.encode(host[d], quality=args.quality)
+        bad = 0
+        ref_dev = [torch.frombuffer(bytearray(refs[d]), dtype=torch.uint8).to(dev) for d in range(D)]
+        for i in range(F):
+            r = ref_dev[i % D]
+            if lens[i] != r.numel() or not torch.equal(outbuf[i * cap:i * cap + lens[i]], r):
+                bad += 1
+        del ref_dev
+        verified = {"frames": F, "distinct_inputs": D, "mismatches": bad,
+                    "method": "every output of the last timed step byte-compared (on the device) with the "
+                              "host-path encode of its input frame"}
+        if bad:
+            raise SystemExit(f"bench: {bad} of {F} outputs differ from the host-path encode")
+
+    # D2H-inclusive pass (device RGB -> .jpg bytes in host memory): the
+    # D distinct frames per step, outputs copied into pinned host buffers.
+    d2h = None
+    if args.d2h_steps > 0:
+        hostout = torch.empty(D * cap, dtype=torch.uint8, pin_memory=True)
+        hfr = frames[:D]
+        hout = [(hostout.data_ptr() + i * cap, cap) for i in range(D)]
+        enc.encode_batch_dev(hfr, hout, quality=args.quality, flags=J.JPGE_DEVICE_INPUT)
+        barrier(pg)
+        t1 = time.perf_counter()
+        for _ in range(args.d2h_steps):
+            hl = enc.encode_batch_dev(hfr, hout, quality=args.quality, flags=J.JPGE_DEVICE_INPUT)
+        d2 = max_over_ranks(pg, time.perf_counter() - t1)
+        d2h_ok = all(hostout[i * cap:i * cap + hl[i]].numpy().tobytes() == refs[i] for i in range(D)) if refs else None
+        d2h = {"value": round(sum_over_ranks(pg, float(W * H * D * args.d2h_steps)) / d2 / 1e6, 1), "unit": "MPix/s",
+               "frames_per_step_per_gpu": D, "steps": args.d2h_steps, "bytes_match": d2h_ok,
+               "what": "device-resident RGB -> finished .jpg bytes in pinned host memory (D2H inside the step)"}
+        del hostout
+
+    # Solo pass (after the timed region, not part of `value`): the distinct frames
+    # through a single-lane encoder with events around every frame's kernels, so each
+    # kernel's duration is its own, without other lanes' kernels beside it.
     tm_solo = None
     solo_win = None
     if args.solo_batches > 0 and not args.no_kernel_events:
         solo = J.Encoder(local, lanes=1)
         solo.set_subsampling(args.subsampling)
-        solo.encode_batch_dev(frames, outd, quality=args.quality)
+        sfr, sout = frames[:D], outd[:D]
+        solo.encode_batch_dev(sfr, sout, quality=args.quality)
         solo.set_timing(1)
         solo.reset_timing()
         s0 = time.monotonic_ns()
         for _ in range(args.solo_batches):
-            solo.encode_batch_dev(frames, outd, quality=args.quality)
+            solo.encode_batch_dev(sfr, sout, quality=args.quality)
         solo_win = [s0, time.monotonic_ns()]
         tm_solo = solo.timing()
         solo.close()
@@ -428,6 +695,12 @@ def main():
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
                          "alg_bytes_per_launch": int(b), "alg_bytes": what, "avg_kernel_ms": round(ms[name], 5),
                          "timed_launches": tm["frames"]}
+        # the north star's "HBM-read roofline": K1's RGB8 read alone (3 B/px)
+        k1 = out["fdct_kernel"]
+        if ms["fdct_kernel"] > 0:
+            rd = 3.0 * npx / (ms["fdct_kernel"] * 1e-3) / 1e9
+            k1["read_achieved"] = round(rd, 1)
+            k1["read_frac"] = round(rd / HBM_PEAK_GBS, 4)
         return out
 
     stages = rooflines(tm)  # in situ: the timed region, lanes side by side
@@ -456,40 +729,60 @@ def main():
             "data": "synthetic (deterministic splitmix64 photo-like frames, HBM-resident)",
             "config": {
                 "workload": f"{W}x{H} {sub_name(args)} Q{args.quality} full encode (RGB8 in HBM -> .jpg bytes in HBM), "
-                            f"{F} distinct frames per GPU per step",
+                            f"{F} frames per GPU per step over {D} distinct inputs",
                 "width": W, "height": H, "quality": args.quality, "subsampling": sub_name(args),
-                "frames_per_step_per_gpu": F,
+                "frames_per_step_per_gpu": F, "distinct_inputs_per_gpu": D,
                 "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
-                "avg_jpeg_bytes": int(total_bytes / (args.steps * F)),
+                "avg_jpeg_bytes": int(avg_jpeg),
             },
             # dominant kernel, timed in situ (HIP events on its lane's stream, lanes side by side)
             "roofline": dict(kernel=dominant, timing="in situ", **stages[dominant]),
-            # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px): the kernel alone
+            # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px; read-only 3 B/px): the kernel alone
             "roofline_dct_stage": dict(kernel="fdct_kernel", timing="solo", **stages_solo["fdct_kernel"])
             if stages_solo else dict(kernel="fdct_kernel", timing="in situ", **stages["fdct_kernel"]),
             "roofline_pipeline": pipeline,
             "stages": stages,
             "stages_solo": stages_solo,
             "kernel_events": f"in situ: HIP events around every {args.event_every}th frame's kernels on its lane's "
-                             f"stream; solo: every frame of {args.solo_batches} batches on a 1-lane encoder after "
-                             f"the timed region",
+                             f"stream; solo: every frame of {args.solo_batches} batches of {D} on a 1-lane encoder "
+                             f"after the timed region",
             "step_ms": {"min": round(min(step_t) * 1e3, 3), "median": round(sorted(step_t)[len(step_t) // 2] * 1e3, 3),
                         "max": round(max(step_t) * 1e3, 3)},
             "lanes": enc.lanes(),
+            "verified": verified,
+            "d2h": d2h,
             # CLOCK_MONOTONIC windows (rocprofv3 timestamps use the same clock): tools/rocprof_window.py
             "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win},
             # host CPU use over the timed region; quota throttling stalls the pipeline
-            "host_cpu": {"cpus_used": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e6 / dt, 2),
-                         "throttled_periods": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
-                         "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3,
-                                               1)} if cg0 else None,
+            "host_cpu": host_cpu_use(cg0, cg1, dt),
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args)
+            cpu, hashes = cpu_baseline(args)
+            if verified is not None and args.subsampling == 420:
+                # the oracle's bytes of the sampled frames against the GPU's (slot i = input i)
+                ok = sum(hashlib.sha256(outbuf[i * cap:i * cap + lens[i]].cpu().numpy().tobytes()).hexdigest() == h
+                         for i, h in hashes.items() if i < D)
+                verified["vs_oracle"] = f"{ok}/{sum(1 for i in hashes if i < D)} sampled frames equal the CPU oracle"
+                if ok != sum(1 for i in hashes if i < D):
+                    raise SystemExit("bench: GPU output differs from the CPU oracle")
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     enc.close()
-    if pg is not None:
-        pg.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args.gpus, argv))  # (the parent never touches a GPU)
+    rank, local, world, pg = dist_setup(args.gpus)
+    run = {"4k-frames": run_frames, "batch1080": run_batch1080, "16k-striped": run_striped16k,
+           "ppm-files": run_ppm_files, "dist-check": run_dist_check}[args.workload]
+    try:
+        run(args, rank, local, world, pg)
+    finally:
+        if pg is not None:
+            pg.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -364,9 +364,11 @@ class Encoder:
         return out[:n.value].tobytes()
 
     def encode_batch_dev(self, frames: list[tuple[int, int, int, int]], outs: list[tuple[int, int]],
-                         quality: int = 50, maxval: int = 255) -> list[int]:
+                         quality: int = 50, maxval: int = 255,
+                         flags: int = JPGE_DEVICE_INPUT | JPGE_DEVICE_OUTPUT) -> list[int]:
         """Pipelined batch on device memory: frames = [(ptr, w, h, stride)], outs = [(ptr, cap)].
-        Returns the .jpg length of each frame (bytes stay in device memory).
+        Returns the .jpg length of each frame (bytes stay in device memory; without
+        JPGE_DEVICE_OUTPUT in `flags` the outs are host pointers, e.g. pinned memory).
         The quality tables and the descriptor array of a repeated batch are reused."""
         q = self._qcache.get(quality)
         if q is None:
@@ -380,8 +382,7 @@ class Encoder:
                 arr[i].out, arr[i].cap = o, cap
             self._desc = (key, arr)
         arr = self._desc[1]
-        st = lib().jpge_encode_batch(self._ctx, arr, len(frames), q[2], q[3],
-                                     JPGE_DEVICE_INPUT | JPGE_DEVICE_OUTPUT)
+        st = lib().jpge_encode_batch(self._ctx, arr, len(frames), q[2], q[3], int(flags))
         _check(st, "encode_batch")
         return [f.len for f in arr]
 

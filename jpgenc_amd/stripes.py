@@ -126,15 +126,26 @@ def encode_stripe_dist(enc, rgb_ptr: int, stride: int, width: int, height: int, 
         v = [int(x) for x in t.cpu().tolist()]
         summaries.append((v[0], tuple(v[1:9]), v[9], v[10], v[11]))
     off, ln, total = enc.stripe_pack(summaries, rank, out.data_ptr(), out.numel())
-    # 4) segments to rank 0 (point-to-point)
+    # 4) segments to rank 0: one grouped round of point-to-point transfers (every
+    #    stripe's xGMI link busy at once), peers named by their global ranks
     spans = [J.stripe_place(summaries, r, hdr_len) for r in range(n)]
     ends = [spans[r + 1][0] if r + 1 < n else total for r in range(n)]
+    ops, staged = [], []
     if rank == 0:
         for r in range(1, n):
             o = spans[r][0]
-            buf = torch.empty(ends[r] - o, dtype=torch.uint8, device=dev)
-            dist.recv(buf, src=r, group=group)
-            out[o:ends[r]].copy_(buf)
+            buf = out[o:ends[r]] if dev == out.device else torch.empty(ends[r] - o, dtype=torch.uint8, device=dev)
+            staged.append((o, buf))
+            ops.append(dist.P2POp(dist.irecv, buf, dist.get_global_rank(group, r) if group is not None else r,
+                                  group=group))
     else:
-        dist.send(out[off:off + ln].to(dev).contiguous(), dst=0, group=group)
+        seg = out[off:off + ln] if dev == out.device else out[off:off + ln].to(dev)
+        ops.append(dist.P2POp(dist.isend, seg, dist.get_global_rank(group, 0) if group is not None else 0,
+                              group=group))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    for o, buf in staged:
+        if buf.device != out.device:
+            out[o:o + buf.numel()].copy_(buf)
     return total

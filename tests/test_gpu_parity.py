@@ -162,7 +162,7 @@ def _large_golden(w, h, quality):
     import json
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_frames.json")) as f:
         for fr in json.load(f)["frames"]:
-            if (fr["width"], fr["height"], fr["quality"]) == (w, h, quality):
+            if (fr["width"], fr["height"], fr["quality"], fr.get("restart", 0)) == (w, h, quality, 0):
                 return fr
     raise KeyError((w, h, quality))
 

@@ -132,3 +132,10 @@ def test_synth_is_deterministic_and_seeded():
 
 
 SYNTH_64x48_SEED1 = "b4196443545c8c8b"
+
+
+def test_quality_tables_match_oracle_every_q():
+    for q in range(1, 101):
+        qy, qc = J.quality_tables(q)
+        oy, oc = _oracle.quality_tables(q)
+        assert np.array_equal(qy, np.asarray(oy, np.uint8)) and np.array_equal(qc, np.asarray(oc, np.uint8)), q

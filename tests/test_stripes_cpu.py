@@ -144,7 +144,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _dist_worker(rank, world, port, seed, q):
+def _dist_worker(rank, world, port, seed, q, members=None):
+    """members: the global ranks of a subgroup that encodes the image (the others
+    only take part in creating the group); None = the whole world."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)
     import torch
@@ -153,30 +155,56 @@ def _dist_worker(rank, world, port, seed, q):
     from jpgenc_amd import stripes as S
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    eng = _FakeStripeEngine(rank, world, seed)
+    group = dist.new_group(members) if members else None
+    if members and rank not in members:
+        q.put((rank, None, None, {}))
+        dist.destroy_process_group()
+        return
+    grank = members.index(rank) if members else rank
+    n = len(members) if members else world
+    eng = _FakeStripeEngine(grank, n, seed)
     out = torch.zeros(len(eng.file) + 64, dtype=torch.uint8)
-    total = S.encode_stripe_dist(eng, 0, 0, 64, 16 * 4 * world, 90, out)
-    ok_file = rank != 0 or bytes(out[:total].numpy().tobytes()) == eng.file
+    total = S.encode_stripe_dist(eng, 0, 0, 64, 16 * 4 * n, 90, out, group=group)
+    ok_file = grank != 0 or bytes(out[:total].numpy().tobytes()) == eng.file
     q.put((rank, total == len(eng.file), ok_file, eng.log))
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(240)
-@pytest.mark.parametrize("seed", [1, 2])
-def test_two_rank_stripe_orchestration(seed):
+def _run_ranks(world, seed, members=None):
     mp = pytest.importorskip("torch.multiprocessing")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, seed, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, seed, q, members)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=200) for _ in procs)
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
-    for rank, ok_total, ok_file, log in res:
+    return res
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("seed", [1, 2])
+def test_two_rank_stripe_orchestration(seed):
+    for rank, ok_total, ok_file, log in _run_ranks(2, seed):
         assert ok_total and ok_file
         assert log["counts_ok"] and log["first_ok"]
         assert log["rows"] == stripes.stripe_rows(8, 2)[rank]
         assert log["seed"] == ([0, 0, 0] if rank == 0 else [1, 2, 3])
+
+
+@pytest.mark.timeout(240)
+def test_stripes_on_a_subgroup():
+    """the image encoded by ranks [1, 2] of a 3-rank world.  The group's
+    rank 0 (global rank 1) must end up with the whole file; peers of the segment
+    gather are global ranks."""
+    res = _run_ranks(3, 3, members=[1, 2])
+    assert res[0][1] is None  # rank 0 is not in the group
+    for rank, ok_total, ok_file, log in res[1:]:
+        g = rank - 1
+        assert ok_total and ok_file
+        assert log["counts_ok"] and log["first_ok"]
+        assert log["rows"] == stripes.stripe_rows(8, 2)[g]
+        assert log["seed"] == ([0, 0, 0] if g == 0 else [1, 2, 3])
