@@ -94,7 +94,9 @@ _LIB = None
 
 
 def lib() -> ctypes.CDLL:
-    """Load libjpge.so (raises if it has not been built)."""
+    """Load libjpge.so (raises if it has not been built).  A process that also uses
+    torch on the GPU must import torch first: torch ships its own HIP runtime, and
+    loaded after libjpge's (ROCm's) it finds no GPU."""
     global _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:  # torch before libjpge: torch brings its own HIP runtime, and a process must load
+    import torch  # noqa: F401  (one copy of it — loaded second, it finds no GPU)
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
