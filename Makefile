@@ -15,14 +15,15 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SR
 CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude
 
-HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp
+HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp coding.cpp
 HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))
-DEV_SRCS  := fdct.hip stats.hip entropy.hip
+DEV_SRCS  := fdct.hip stats.hip entropy.hip planes.hip
 DEV_OBJS  := $(addprefix $(BUILD)/,$(DEV_SRCS:.hip=.o))
 DIAG_OBJS := $(addprefix $(BUILD)/diag/,$(DEV_SRCS:.hip=.o))
 HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h
+FACADE_TEST := tests/cpp/bin/test_facade
 
-all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc oracle
+all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) oracle
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HEADERS)
 	@mkdir -p $(BUILD)
@@ -56,7 +57,14 @@ diag: $(DIAG_OBJS) $(HOST_OBJS)
 	  -L$(ROCM)/lib -lamdhip64
 
 clean:
-	rm -rf build $(LIBDIR) $(BINDIR)
+	rm -rf build $(LIBDIR) $(BINDIR) tests/cpp/bin
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# the facade under the reference's unit tests (tests/cpp/test_facade.cpp; run by
+# tests/test_facade.py): compiled exactly as reference code would be, global names
+$(FACADE_TEST): tests/cpp/test_facade.cpp $(LIBDIR)/libjpge.so $(SRC)/jpge_image.hpp include/jpge.h
+	@mkdir -p tests/cpp/bin
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -ljpge -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' \
+	  -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib

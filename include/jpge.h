@@ -8,8 +8,9 @@
  *
  * Conventions: every function returns a jpge_status (0 = ok); no exceptions or
  * C++ types cross this boundary; all buffers are owned by the caller; a context
- * (one HIP device + its streams and workspace) must not be used from two
- * threads at once.  Output bytes are bit-identical to the reference encoder.
+ * (one HIP device + its streams and workspace) may be shared between threads: its
+ * calls run one at a time (each call holds the context).  Output bytes are
+ * bit-identical to the reference encoder.
  */
 #ifndef JPGE_H_
 #define JPGE_H_
@@ -215,6 +216,74 @@ int jpge_synth_rgb8(uint64_t seed, uint32_t width, uint32_t height, int kind, ui
 /* The Arai constants compiled into the kernels (Dct.hpp:21-43), for verification:
  * a[0..4] = a1..a5, s[0..7] = s0..s7. */
 void jpge_arai_constants(double a[5], double s[8]);
+
+/* ---- Coding.hpp primitives (host; per block, as the reference's free functions) ----
+ * The GPU path computes all of these inside its kernels; these entries serve the
+ * facade's Coding.hpp functions (jpge_image.hpp) and their known-answer tests. */
+
+/* zigzag(int) (Coding.hpp:57-81): the natural (row-major) index of zig-zag position
+ * i (0..63); -1 for i outside 0..63 (the reference asserts). */
+int jpge_zigzag_index(int i);
+/* zigzag(matrix) (Coding.hpp:30-54): out[zig-zag position of (r, c)] = in[r * 8 + c]. */
+int jpge_zigzag_block(const int32_t in[64], int32_t out[64]);
+/* quantize (Coding.hpp:84-97): out[i] = (int)round(block[i] / table[i]), row-major. */
+int jpge_quantize_block(const double block[64], const double table[64], int32_t out[64]);
+/* RLE_AC (Coding.hpp:112-183): (run, value) pairs; pair 0 is (0, DC); a value after
+ * more than 15 zeros is preceded by (15, 0) pairs; a trailing zero run ends with the
+ * EOB pair (0, 0).  zigzag_scan = 0: the vector version over data[0..n) as given
+ * (n >= 2); 1: the matrix version over a natural-order 8x8 block (n = 64) scanned in
+ * zig-zag order.  *npairs receives the count (JPGE_E_NOSPACE if cap is smaller). */
+int jpge_rle_ac(const int32_t* data, size_t n, int zigzag_scan, uint8_t* runs, int32_t* values, size_t cap,
+                size_t* npairs);
+/* getCategoryAndCode (Coding.hpp:197-262): category = bit length of |value| (0 for
+ * 0), bits = value if > 0 else (2^category - 1) - |value| (the low `category` bits,
+ * written MSB-first).  JPGE_E_RANGE for |value| >= 2^15 (the reference asserts). */
+int jpge_category_code(int32_t value, uint16_t* category, uint32_t* bits);
+/* encode_category (Coding.hpp:265-283): per pair, symbol = (run << 4) | category and
+ * its extra bits (code, code_lens[i] = category). */
+int jpge_encode_category(const uint8_t* runs, const int32_t* values, size_t n, uint8_t* symbols, uint32_t* codes,
+                         uint8_t* code_lens);
+/* applyDCdifferenceCoding (Image.cpp:638-678), in place on quantised int planes:
+ * the Y DCs in MCU order (2x2 blocks of 8x8 per 16x16 MCU), each chroma plane's DCs
+ * in block raster order; every chain starts at 0.  Y is rows x cols (multiples of
+ * 16), the chroma planes crows x ccols (multiples of 8). */
+int jpge_dc_difference(int32_t* y, uint32_t rows, uint32_t cols, int32_t* cb, int32_t* cr, uint32_t crows,
+                       uint32_t ccols);
+
+/* ---- Plane stages: the reference's Image stage methods on fp64 planes (GPU) ----
+ * Row-major planes of doubles (Image's matrix<PixelDataType>); host buffers, or
+ * device buffers with JPGE_DEVICE_INPUT / JPGE_DEVICE_OUTPUT.  Each call returns with
+ * its results in place.  Bit-identical to the reference's loops. */
+#define JPGE_TO_RGB 0
+#define JPGE_TO_YCBCR 1
+/* convertToColorSpace (Image.cpp:112-179) of n pixels: JPGE_TO_YCBCR takes R,G,B
+ * planes to Y,Cb,Cr; JPGE_TO_RGB the reverse. */
+int jpge_color_convert(jpge_ctx* ctx, const double* in0, const double* in1, const double* in2, double* out0,
+                       double* out1, double* out2, size_t n, int target, uint32_t flags);
+/* Image::subsample with applySubsampling's mask for `mode` (JPGE_S*; Image.cpp:
+ * 198-319) on one rows x cols plane; out gets out_rows x out_cols (S444: a copy).
+ * out = NULL: only the output size. */
+int jpge_subsample_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int mode, double* out,
+                         uint32_t* out_rows, uint32_t* out_cols, uint32_t flags);
+#define JPGE_DCT_SIMPLE 0 /* dctDirect (Dct.hpp:238-262) */
+#define JPGE_DCT_MATRIX 1 /* dctMat (Dct.hpp:264-276) */
+#define JPGE_DCT_ARAI 2   /* dctArai (Dct.hpp:47-215), writeJPEG's */
+/* applyDCT(mode) (Image.cpp:540-595) on one plane of 8x8 blocks (rows, cols
+ * multiples of 8). */
+int jpge_dct_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int dct_mode, double* out,
+                   uint32_t flags);
+/* applyQuantization's per-block quantize (Image.cpp:597-636, Coding.hpp:84-97) on
+ * one plane of 8x8 blocks with one natural-order table. */
+int jpge_quantize_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, const uint8_t table[64],
+                        int32_t* out, uint32_t flags);
+/* writeJPEG (Image.cpp:831-976) on an Image's three planes (rows x cols, multiples of
+ * 16): colorspace JPGE_TO_RGB = the planes are R,G,B (converted first), JPGE_TO_YCBCR
+ * = they are Y,Cb,Cr with full-size chroma; then S420_m, Arai, quantisation, DC/RLE/
+ * category, per-image tables and emission, all on the GPU.  SOF0 carries
+ * real_width x real_height.  The context's restart interval applies. */
+int jpge_encode_planes(jpge_ctx* ctx, const double* p0, const double* p1, const double* p2, uint32_t rows,
+                       uint32_t cols, int colorspace, uint32_t real_width, uint32_t real_height, const uint8_t qy[64],
+                       const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len, uint32_t flags);
 
 /* ---- Row stripes of one large image across devices ----
  * The image (width x height, 4:2:0) is cut into stripes of whole MCU rows (16 px);

@@ -40,7 +40,13 @@ EXPORTS = (
     "jpge_ppm_info", "jpge_encode_file", "jpge_encode_files", "jpge_synth_rgb8", "jpge_arai_constants",
     "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
     "jpge_huffman_decode", "jpge_idct8x8", "jpge_decode_coeffs",
+    "jpge_zigzag_index", "jpge_zigzag_block", "jpge_quantize_block", "jpge_rle_ac", "jpge_category_code",
+    "jpge_encode_category", "jpge_dc_difference", "jpge_color_convert", "jpge_subsample_plane", "jpge_dct_plane",
+    "jpge_quantize_plane", "jpge_encode_planes",
 )
+
+JPGE_TO_RGB, JPGE_TO_YCBCR = 0, 1
+DCT_SIMPLE, DCT_MATRIX, DCT_ARAI = 0, 1, 2
 
 
 class JpgeError(RuntimeError):
@@ -144,6 +150,19 @@ def lib() -> ctypes.CDLL:
         L.jpge_idct8x8.argtypes = [vp, vp]
         L.jpge_idct8x8.restype = None
         L.jpge_decode_coeffs.argtypes = [vp, sz, ctypes.POINTER(Decoded), vp, vp, vp, sz, sz]
+        L.jpge_zigzag_index.argtypes = [i32]
+        L.jpge_zigzag_block.argtypes = [vp, vp]
+        L.jpge_quantize_block.argtypes = [vp, vp, vp]
+        L.jpge_rle_ac.argtypes = [vp, sz, i32, vp, vp, sz, ctypes.POINTER(sz)]
+        L.jpge_category_code.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(u32)]
+        L.jpge_encode_category.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.jpge_dc_difference.argtypes = [vp, u32, u32, vp, vp, u32, u32]
+        L.jpge_color_convert.argtypes = [vp, vp, vp, vp, vp, vp, vp, sz, i32, u32]
+        L.jpge_subsample_plane.argtypes = [vp, vp, u32, u32, i32, vp, ctypes.POINTER(u32), ctypes.POINTER(u32), u32]
+        L.jpge_dct_plane.argtypes = [vp, vp, u32, u32, i32, vp, u32]
+        L.jpge_quantize_plane.argtypes = [vp, vp, u32, u32, vp, vp, u32]
+        L.jpge_encode_planes.argtypes = [vp, vp, vp, vp, u32, u32, i32, u32, u32, vp, vp, vp, sz, ctypes.POINTER(sz),
+                                         u32]
         _LIB = L
     return _LIB
 
@@ -266,6 +285,67 @@ def huffman_table(counts, first):
     _check(lib().jpge_huffman_table(_p(c), _p(f), _p(bits), _p(hv), ctypes.byref(n), _p(code), _p(ln)),
            "huffman_table")
     return bits, hv[:n.value].tolist(), code, ln
+
+
+# ---- Coding.hpp primitives (host, C ABI) ----
+def zigzag_index(i: int) -> int:
+    """zigzag(int) (Coding.hpp:57-81): natural index of zig-zag position i (-1 outside 0..63)."""
+    return int(lib().jpge_zigzag_index(int(i)))
+
+
+def zigzag_block(block) -> np.ndarray:
+    """zigzag(matrix) (Coding.hpp:30-54) of a natural-order 8x8 block."""
+    a = np.ascontiguousarray(block, np.int32).reshape(64)
+    out = np.zeros(64, np.int32)
+    _check(lib().jpge_zigzag_block(_p(a), _p(out)), "zigzag_block")
+    return out
+
+
+def quantize_block(block, table) -> np.ndarray:
+    """quantize (Coding.hpp:84-97): round-half-away of block / table, natural order."""
+    b = np.ascontiguousarray(block, np.float64).reshape(64)
+    t = np.ascontiguousarray(table, np.float64).reshape(64)
+    out = np.zeros(64, np.int32)
+    _check(lib().jpge_quantize_block(_p(b), _p(t), _p(out)), "quantize_block")
+    return out.reshape(8, 8)
+
+
+def rle_ac(data, zigzag_scan: bool = False) -> list[tuple[int, int]]:
+    """RLE_AC (Coding.hpp:112-183): [(run, value)]; zigzag_scan: the 8x8 matrix version."""
+    d = np.ascontiguousarray(data, np.int32).reshape(-1)
+    runs = np.zeros(d.size + 64, np.uint8)
+    vals = np.zeros(d.size + 64, np.int32)
+    n = ctypes.c_size_t()
+    _check(lib().jpge_rle_ac(_p(d), d.size, int(zigzag_scan), _p(runs), _p(vals), runs.size, ctypes.byref(n)),
+           "rle_ac")
+    return list(zip(runs[:n.value].tolist(), vals[:n.value].tolist()))
+
+
+def category_code(value: int) -> tuple[int, int]:
+    """getCategoryAndCode (Coding.hpp:197-262): (category, extra bits)."""
+    c, b = ctypes.c_uint16(), ctypes.c_uint32()
+    _check(lib().jpge_category_code(int(value), ctypes.byref(c), ctypes.byref(b)), "category_code")
+    return c.value, b.value
+
+
+def encode_category(pairs) -> list[tuple[int, int, int]]:
+    """encode_category (Coding.hpp:265-283): [(symbol, extra bits, bit count)]."""
+    n = len(pairs)
+    runs = np.ascontiguousarray([p[0] for p in pairs] or [0], np.uint8)
+    vals = np.ascontiguousarray([p[1] for p in pairs] or [0], np.int32)
+    syms, lens = np.zeros(max(1, n), np.uint8), np.zeros(max(1, n), np.uint8)
+    codes = np.zeros(max(1, n), np.uint32)
+    _check(lib().jpge_encode_category(_p(runs), _p(vals), n, _p(syms), _p(codes), _p(lens)), "encode_category")
+    return list(zip(syms[:n].tolist(), codes[:n].tolist(), lens[:n].tolist()))
+
+
+def dc_difference(qy: np.ndarray, qcb: np.ndarray, qcr: np.ndarray) -> None:
+    """applyDCdifferenceCoding (Image.cpp:638-678) in place on int32 planes."""
+    for a in (qy, qcb, qcr):
+        if a.dtype != np.int32 or not a.flags.c_contiguous:
+            raise ValueError("int32 C-contiguous planes expected")
+    _check(lib().jpge_dc_difference(_p(qy), qy.shape[0], qy.shape[1], _p(qcb), _p(qcr), qcb.shape[0], qcb.shape[1]),
+           "dc_difference")
 
 
 def arai_constants() -> tuple[np.ndarray, np.ndarray]:
@@ -446,6 +526,56 @@ class Encoder:
         _check(lib().jpge_stripe_pack(self._ctx, arr, len(summaries), index, out_ptr, cap, ctypes.byref(off),
                                       ctypes.byref(ln), ctypes.byref(tot)), "stripe_pack")
         return off.value, ln.value, tot.value
+
+    # ---- plane stages: the reference's Image stage methods on fp64 planes (GPU) ----
+    def color_convert(self, p0, p1, p2, target: int = JPGE_TO_YCBCR):
+        """convertToColorSpace (Image.cpp:112-179) of three equal-size planes."""
+        ins = [np.ascontiguousarray(p, np.float64) for p in (p0, p1, p2)]
+        outs = [np.empty_like(ins[0]) for _ in range(3)]
+        _check(lib().jpge_color_convert(self._ctx, *[_p(a) for a in ins], *[_p(a) for a in outs], ins[0].size,
+                                        int(target), 0), "color_convert")
+        return outs
+
+    def subsample_plane(self, plane, mode: int) -> np.ndarray:
+        """Image::subsample with applySubsampling's mask for `mode` (jpge.h JPGE_S*)."""
+        a = np.ascontiguousarray(plane, np.float64)
+        r, c = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().jpge_subsample_plane(self._ctx, _p(a), a.shape[0], a.shape[1], int(mode), None, ctypes.byref(r),
+                                          ctypes.byref(c), 0), "subsample_plane")
+        out = np.empty((r.value, c.value), np.float64)
+        _check(lib().jpge_subsample_plane(self._ctx, _p(a), a.shape[0], a.shape[1], int(mode), _p(out),
+                                          ctypes.byref(r), ctypes.byref(c), 0), "subsample_plane")
+        return out
+
+    def dct_plane(self, plane, mode: int = DCT_ARAI) -> np.ndarray:
+        """applyDCT(mode) (Image.cpp:540-595) on one plane of 8x8 blocks."""
+        a = np.ascontiguousarray(plane, np.float64)
+        out = np.empty_like(a)
+        _check(lib().jpge_dct_plane(self._ctx, _p(a), a.shape[0], a.shape[1], int(mode), _p(out), 0), "dct_plane")
+        return out
+
+    def quantize_plane(self, plane, table) -> np.ndarray:
+        """applyQuantization's per-block quantize (Coding.hpp:84-97) with one table."""
+        a = np.ascontiguousarray(plane, np.float64)
+        t = np.ascontiguousarray(table, np.uint8).reshape(64)
+        out = np.empty(a.shape, np.int32)
+        _check(lib().jpge_quantize_plane(self._ctx, _p(a), a.shape[0], a.shape[1], _p(t), _p(out), 0),
+               "quantize_plane")
+        return out
+
+    def encode_planes(self, p0, p1, p2, real_width: int, real_height: int, colorspace: int = JPGE_TO_RGB,
+                      quality: int = 50) -> bytes:
+        """writeJPEG (Image.cpp:831-976) on an Image's three fp64 planes (rows x cols,
+        multiples of 16): R,G,B (colorspace JPGE_TO_RGB) or Y,Cb,Cr (JPGE_TO_YCBCR)."""
+        ins = [np.ascontiguousarray(p, np.float64) for p in (p0, p1, p2)]
+        rows, cols = ins[0].shape
+        qy, qc = self._tables(quality, None, None)
+        out = np.empty(max_jpeg_bytes(cols, rows), np.uint8)
+        n = ctypes.c_size_t()
+        _check(lib().jpge_encode_planes(self._ctx, *[_p(a) for a in ins], rows, cols, int(colorspace), real_width,
+                                        real_height, _p(qy), _p(qc), _p(out), out.size, ctypes.byref(n), 0),
+               "encode_planes")
+        return out[:n.value].tobytes()
 
     def encode_file(self, ppm_path: str, jpg_path: str, quality: int = 50) -> None:
         """main.cpp: loadPPM(ppm_path) + writeJPEG(jpg_path)."""

@@ -300,3 +300,45 @@ int jpge_stripe_pack(jpge_ctx* ctx, const jpge_stripe_summary* all, int n, int i
 }
 
 }  // extern "C"
+
+// ---- plane stages (the facade's Image stage methods on the GPU) ----
+extern "C" {
+
+int jpge_color_convert(jpge_ctx* ctx, const double* in0, const double* in1, const double* in2, double* out0,
+                       double* out1, double* out2, size_t n, int target, uint32_t flags) {
+    if (!ctx || (target != JPGE_TO_RGB && target != JPGE_TO_YCBCR)) return JPGE_E_ARG;
+    const double* in[3] = {in0, in1, in2};
+    double* out[3] = {out0, out1, out2};
+    return ctx->enc->stage_color(in, out, n, target == JPGE_TO_YCBCR, flags);
+}
+
+int jpge_subsample_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int mode, double* out,
+                         uint32_t* out_rows, uint32_t* out_cols, uint32_t flags) {
+    if (!ctx) return JPGE_E_ARG;
+    if (const int e = jpge::Encoder::subsample_shape(mode, rows, cols, out_rows, out_cols)) return e;
+    if (!out) return JPGE_OK;
+    return ctx->enc->stage_subsample(in, rows, cols, mode, out, flags);
+}
+
+int jpge_dct_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int dct_mode, double* out,
+                   uint32_t flags) {
+    if (!ctx) return JPGE_E_ARG;
+    return ctx->enc->stage_dct(in, rows, cols, dct_mode, out, flags);
+}
+
+int jpge_quantize_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, const uint8_t table[64],
+                        int32_t* out, uint32_t flags) {
+    if (!ctx) return JPGE_E_ARG;
+    return ctx->enc->stage_quantize(in, rows, cols, table, out, flags);
+}
+
+int jpge_encode_planes(jpge_ctx* ctx, const double* p0, const double* p1, const double* p2, uint32_t rows,
+                       uint32_t cols, int colorspace, uint32_t real_width, uint32_t real_height, const uint8_t qy[64],
+                       const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len, uint32_t flags) {
+    if (!ctx || (colorspace != JPGE_TO_RGB && colorspace != JPGE_TO_YCBCR)) return JPGE_E_ARG;
+    const double* p[3] = {p0, p1, p2};
+    return ctx->enc->encode_planes(p, rows, cols, colorspace == JPGE_TO_YCBCR, real_width, real_height, qy, qc, out,
+                                   cap, len, flags);
+}
+
+}  // extern "C"

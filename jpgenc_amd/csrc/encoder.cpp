@@ -5,6 +5,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
@@ -397,6 +398,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
 
 Encoder::~Encoder() {
     for (auto& ln : lanes_) ln->shutdown();
+    for (auto& b : scratch_) hipFree(b.first);
     pool_.reset();  // (no jobs are pending between calls)
     hipSetDevice(device_);
     for (auto& ln : lanes_) {
@@ -685,6 +687,7 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
 }
 
 int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags, nullptr, true);
@@ -698,6 +701,7 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
 }
 
 int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     const auto t_enter = std::chrono::steady_clock::now();
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
@@ -880,6 +884,7 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
 
 int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                         int16_t* y, int16_t* cb, int16_t* cr) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
@@ -905,6 +910,7 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
 
 int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                           uint32_t counts[1024], uint64_t first[1024]) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
@@ -926,6 +932,7 @@ int Encoder::symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_
 // padding replicates the image's last row, Image.cpp:511-519).  Every phase runs on
 // lane 0's first slot and returns when its results are on the host.
 int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const uint8_t qc[64], int32_t last_dc[3]) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     if (!d.rgb || !last_dc || d.width == 0 || d.height == 0 || d.width > 65535 || d.height > 65535) return kErrArg;
     if (mode_ != 420) return kErrArg;  // stripes are S420_m (the reference's subsampling)
@@ -968,6 +975,7 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
 }
 
 int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t first[1024]) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !seed || !counts || !first) return kErrArg;
@@ -988,6 +996,7 @@ int Encoder::stripe_stats(const int32_t seed[3], uint32_t counts[1024], uint64_t
 
 int Encoder::stripe_code(const uint32_t counts[1024], const uint64_t first[1024], StripeSummary* sum,
                          size_t* hdr_len) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !counts || !first || !sum) return kErrArg;
@@ -1053,6 +1062,7 @@ int Encoder::stripe_place(const StripeSummary* all, int n, int index, size_t hdr
 
 int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* out_dev, size_t cap, size_t* seg_off,
                          size_t* seg_len, size_t* total_len) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     if (!s.in_dev || !out_dev || !s.hdr_len) return kErrArg;
@@ -1083,6 +1093,312 @@ int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* ou
     if (seg_len) *seg_len = end - off;
     if (total_len) *total_len = total;
     return (index == n - 1 && end != total) ? kErrInternal : kOk;
+}
+
+// ---- plane stages (the facade's Image stage methods; planes.hip) ----
+
+void* Encoder::scratch(int i, size_t bytes) {
+    if ((int)scratch_.size() <= i) scratch_.resize(i + 1, {nullptr, 0});
+    auto& b = scratch_[i];
+    if (b.second < bytes) {
+        hipFree(b.first);
+        b = {nullptr, 0};
+        if (hipMalloc(&b.first, bytes) != hipSuccess) return nullptr;
+        b.second = bytes;
+    }
+    return b.first;
+}
+
+#define JPGE_SCRATCH(var, idx, bytes)                     \
+    void* var = scratch((idx), (bytes));                  \
+    if (!var) return kErrHip
+
+int Encoder::stage_color(const double* const in[3], double* const out[3], size_t n, int to_ycc, uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
+    JPGE_HIP(hipSetDevice(device_));
+    for (int c = 0; c < 3; ++c)
+        if (!in[c] || !out[c]) return kErrArg;
+    if (n == 0) return kOk;
+    hipStream_t st = lanes_[0]->stream;
+    const size_t bytes = n * 8;
+    PlaneColorArgs a;
+    const double* din[3];
+    double* dout[3];
+    for (int c = 0; c < 3; ++c) {
+        if (flags & kFlagDeviceInput) {
+            din[c] = in[c];
+        } else {
+            JPGE_SCRATCH(b, c, bytes);
+            JPGE_HIP(hipMemcpyAsync(b, in[c], bytes, hipMemcpyHostToDevice, st));
+            din[c] = static_cast<const double*>(b);
+        }
+        if (flags & kFlagDeviceOutput) {
+            dout[c] = out[c];
+        } else {
+            JPGE_SCRATCH(b, 3 + c, bytes);
+            dout[c] = static_cast<double*>(b);
+        }
+    }
+    a.in0 = din[0]; a.in1 = din[1]; a.in2 = din[2];
+    a.out0 = dout[0]; a.out1 = dout[1]; a.out2 = dout[2];
+    a.n = n;
+    a.to_ycc = to_ycc;
+    JPGE_HIP(launch_plane_color(a, st));
+    if (!(flags & kFlagDeviceOutput))
+        for (int c = 0; c < 3; ++c) JPGE_HIP(hipMemcpyAsync(out[c], dout[c], bytes, hipMemcpyDeviceToHost, st));
+    JPGE_HIP(hipStreamSynchronize(st));
+    return kOk;
+}
+
+// applySubsampling's masks (Image.cpp:256-309) as PlaneSubsampleArgs; S444 leaves
+// the plane as it is.
+static bool subsample_mask(int mode, PlaneSubsampleArgs& a, uint32_t& vdiv) {
+    a.mask[0] = 1; a.mask[1] = 0; a.mask[2] = 0; a.mask[3] = 0;
+    a.m = 2; a.row_step = 2; a.avg_div = 0; vdiv = 2;
+    switch (mode) {
+        case 444: a.m = 1; a.row_step = 1; vdiv = 1; return true;
+        case 422: a.row_step = 1; vdiv = 1; return true;               // {1, 0}
+        case 411: a.m = 4; a.row_step = 1; vdiv = 1; return true;      // {1, 0, 0, 0}
+        case 4200: return true;                                         // {1, 0}, scanline jump
+        case 420: a.mask[1] = 1; a.avg_div = 4; return true;           // {1, 1}, averaging / 4
+        case 4201: a.avg_div = 2; return true;                         // {1, 0}, averaging / 2
+        default: return false;
+    }
+}
+
+int Encoder::subsample_shape(int mode, uint32_t rows, uint32_t cols, uint32_t* out_rows, uint32_t* out_cols) {
+    PlaneSubsampleArgs a;
+    uint32_t vdiv;
+    if (!subsample_mask(mode, a, vdiv)) return kErrArg;
+    // the reference's loop reads whole mask runs and, in pairs, the next scanline
+    if (rows == 0 || cols == 0 || cols % a.m || (a.row_step == 2 && rows % 2)) return kErrArg;
+    if (out_rows) *out_rows = rows / vdiv;
+    if (out_cols) *out_cols = cols / a.m;
+    return kOk;
+}
+
+int Encoder::stage_subsample(const double* in, uint32_t rows, uint32_t cols, int mode, double* out, uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
+    JPGE_HIP(hipSetDevice(device_));
+    PlaneSubsampleArgs a;
+    uint32_t vdiv, orows, ocols;
+    if (!in || !out || !subsample_mask(mode, a, vdiv)) return kErrArg;
+    if (const int e = subsample_shape(mode, rows, cols, &orows, &ocols)) return e;
+    hipStream_t st = lanes_[0]->stream;
+    const size_t ib = (size_t)rows * cols * 8, ob = (size_t)orows * ocols * 8;
+    const double* din = in;
+    if (!(flags & kFlagDeviceInput)) {
+        JPGE_SCRATCH(b, 0, ib);
+        JPGE_HIP(hipMemcpyAsync(b, in, ib, hipMemcpyHostToDevice, st));
+        din = static_cast<const double*>(b);
+    }
+    double* dout = out;
+    if (!(flags & kFlagDeviceOutput)) {
+        JPGE_SCRATCH(b, 1, ob);
+        dout = static_cast<double*>(b);
+    }
+    if (mode == 444) {
+        JPGE_HIP(hipMemcpyAsync(dout, din, ib, hipMemcpyDeviceToDevice, st));
+    } else {
+        a.in = din;
+        a.out = dout;
+        a.cols = cols;
+        a.out_rows = orows;
+        a.out_cols = ocols;
+        JPGE_HIP(launch_plane_subsample(a, st));
+    }
+    if (!(flags & kFlagDeviceOutput)) JPGE_HIP(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, st));
+    JPGE_HIP(hipStreamSynchronize(st));
+    return kOk;
+}
+
+// Dct.hpp:220-235: A(k, n) = C0(k) sqrt(2/8) cos((2n+1) (k pi / 16)), glibc cos on the host
+static void dct_matrix_a(double A[64]) {
+    const double pi = 0x1.921fb54442d18p+1, root_two = 0x1.6a09e667f3bcdp+0;
+    const double scale = std::sqrt(2. / 8);
+    for (int k = 0; k < 8; ++k)
+        for (int n = 0; n < 8; ++n) {
+            const double cos_term = (2. * n + 1.) * ((k * pi) / (2. * 8));
+            A[k * 8 + n] = (k == 0 ? 1. / root_two : 1.) * scale * std::cos(cos_term);
+        }
+}
+
+int Encoder::stage_dct(const double* in, uint32_t rows, uint32_t cols, int dct_mode, double* out, uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
+    JPGE_HIP(hipSetDevice(device_));
+    if (!in || !out || rows % 8 || cols % 8 || dct_mode < kDctSimple || dct_mode > kDctArai) return kErrArg;
+    if (rows == 0 || cols == 0) return kOk;
+    hipStream_t st = lanes_[0]->stream;
+    const size_t bytes = (size_t)rows * cols * 8;
+    const double* din = in;
+    if (!(flags & kFlagDeviceInput)) {
+        JPGE_SCRATCH(b, 0, bytes);
+        JPGE_HIP(hipMemcpyAsync(b, in, bytes, hipMemcpyHostToDevice, st));
+        din = static_cast<const double*>(b);
+    }
+    double* dout = out;
+    if (!(flags & kFlagDeviceOutput)) {
+        JPGE_SCRATCH(b, 1, bytes);
+        dout = static_cast<double*>(b);
+    }
+    PlaneBlockArgs a{};
+    a.in0 = din;
+    a.cols = cols;
+    a.nblocks = (uint64_t)(rows / 8) * (cols / 8);
+    a.sink = kSinkDouble;
+    dct_matrix_a(a.A);
+    a.out_d = dout;
+    JPGE_HIP(launch_plane_block(a, dct_mode, st));
+    if (!(flags & kFlagDeviceOutput)) JPGE_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, st));
+    JPGE_HIP(hipStreamSynchronize(st));
+    return kOk;
+}
+
+int Encoder::stage_quantize(const double* in, uint32_t rows, uint32_t cols, const uint8_t table[64], int32_t* out,
+                            uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
+    JPGE_HIP(hipSetDevice(device_));
+    if (!in || !out || !table || rows % 8 || cols % 8) return kErrArg;
+    if (rows == 0 || cols == 0) return kOk;
+    hipStream_t st = lanes_[0]->stream;
+    const size_t n = (size_t)rows * cols;
+    const double* din = in;
+    if (!(flags & kFlagDeviceInput)) {
+        JPGE_SCRATCH(b, 0, n * 8);
+        JPGE_HIP(hipMemcpyAsync(b, in, n * 8, hipMemcpyHostToDevice, st));
+        din = static_cast<const double*>(b);
+    }
+    int32_t* dout = out;
+    if (!(flags & kFlagDeviceOutput)) {
+        JPGE_SCRATCH(b, 1, n * 4);
+        dout = static_cast<int32_t*>(b);
+    }
+    PlaneQuantArgs a;
+    a.in = din;
+    a.out = dout;
+    a.rows = rows;
+    a.cols = cols;
+    for (int i = 0; i < 64; ++i) a.q[i] = table[i];
+    JPGE_HIP(launch_plane_quant(a, st));
+    if (!(flags & kFlagDeviceOutput)) JPGE_HIP(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
+    JPGE_HIP(hipStreamSynchronize(st));
+    return kOk;
+}
+
+int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_t cols, int ycc, uint32_t real_w,
+                           uint32_t real_h, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
+                           size_t* len, uint32_t flags) {
+    std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
+    JPGE_HIP(hipSetDevice(device_));
+    for (int c = 0; c < 3; ++c)
+        if (!planes[c]) return kErrArg;
+    if (!out || !len || !qy || !qc || rows == 0 || cols == 0 || rows % 16 || cols % 16 || rows > 65536 ||
+        cols > 65536 || real_w == 0 || real_h == 0 || real_w > 65535 || real_h > 65535)
+        return kErrArg;
+    for (int i = 0; i < 64; ++i)
+        if (!qy[i] || !qc[i]) return kErrArg;
+    Slot& s = *lanes_[0]->slots[0];
+    hipStream_t st = s.stream;
+    // the frame as writeJPEG sees it: S420_m MCUs over the planes (rows, cols already
+    // whole MCUs: loadPPM pads to 16, Image.cpp:480-531); SOF0 carries the real size
+    Geometry g = geometry(cols, rows, 420);
+    const size_t out_cap = (flags & kFlagDeviceOutput) ? 0 : max_jpeg_bytes(cols, rows);
+    if (const int e = ensure(s, g, 0, out_cap)) return e;
+    const size_t n = (size_t)rows * cols, bytes = n * 8;
+    const double* p[3];
+    for (int c = 0; c < 3; ++c) {
+        if (flags & kFlagDeviceInput) {
+            p[c] = planes[c];
+        } else {
+            JPGE_SCRATCH(b, c, bytes);
+            JPGE_HIP(hipMemcpyAsync(b, planes[c], bytes, hipMemcpyHostToDevice, st));
+            p[c] = static_cast<const double*>(b);
+        }
+    }
+    if (!ycc) {  // *this = convertToColorSpace(YCbCr), Image.cpp:839
+        double* q[3];
+        for (int c = 0; c < 3; ++c) {
+            JPGE_SCRATCH(b, 3 + c, bytes);
+            q[c] = static_cast<double*>(b);
+        }
+        PlaneColorArgs a;
+        a.in0 = p[0]; a.in1 = p[1]; a.in2 = p[2];
+        a.out0 = q[0]; a.out1 = q[1]; a.out2 = q[2];
+        a.n = n;
+        a.to_ycc = 1;
+        JPGE_HIP(launch_plane_color(a, st));
+        for (int c = 0; c < 3; ++c) p[c] = q[c];
+    }
+    // applySubsampling(S420_m), Image.cpp:842 (Cr, then Cb: independent planes)
+    const double* sub[2];
+    for (int c = 0; c < 2; ++c) {
+        PlaneSubsampleArgs a;
+        uint32_t vdiv;
+        subsample_mask(420, a, vdiv);
+        JPGE_SCRATCH(b, 6 + c, bytes / 4);
+        a.in = p[1 + c];
+        a.out = static_cast<double*>(b);
+        a.cols = cols;
+        a.out_rows = rows / 2;
+        a.out_cols = cols / 2;
+        JPGE_HIP(launch_plane_subsample(a, st));
+        sub[c] = a.out;
+    }
+    std::memcpy(s.qy, qy, 64);
+    std::memcpy(s.qc, qc, 64);
+    s.g = g;
+    s.in_dev = reinterpret_cast<const uint8_t*>(p[0]);  // (marks the slot in use; K1 is not run)
+    s.in_stride = 0;
+    if (flags & kFlagDeviceOutput) {
+        s.out_dev = out;
+        s.out_cap = cap;
+    } else {
+        s.out_dev = s.d_out;
+        s.out_cap = s.cap_out;
+    }
+    s.seed = DcSeed();
+    s.rst = Restart();
+    s.rst.mcus = restart_mcus_;
+    s.key_y0 = s.key_c0 = s.key_ncb = 0;
+    s.img_w = real_w;
+    s.img_h = real_h;
+    s.timed = false;
+    s.tables_done.store(0, std::memory_order_relaxed);
+    s.export_queued.store(0, std::memory_order_relaxed);
+    // applyDCT(Arai) + applyQuantization (Image.cpp:844-871) into the MCU layout; the
+    // control block is zeroed here (K1 does it on the RGB8 path)
+    const CtlLayout L(layout(g).grid());
+    JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, L.total, st));
+    PlaneBlockArgs b{};
+    b.in0 = p[0];
+    b.in1 = sub[0];
+    b.in2 = sub[1];
+    b.cols = cols;
+    b.nblocks = (uint64_t)g.nblocks();
+    b.mcu = 1;
+    b.sink = kSinkMcu16;
+    for (int i = 0; i < 64; ++i) {
+        b.q[i] = qy[i];
+        b.q[64 + i] = qc[i];
+    }
+    b.out_h = s.d_coef;
+    JPGE_HIP(launch_plane_block(b, kDctArai, st));
+    const StatsArgs st2 = stats_args(s);
+    JPGE_HIP(launch_stats(st2, st));
+    s.seq = ++seq_counter_;
+    s.hist = st2.hist;
+    JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq, st));
+    s.export_queued.store(1, std::memory_order_release);
+    FrameDesc f;
+    f.out = out;
+    f.cap = cap;
+    int e = build_tables(s, true);
+    if (!e) e = import_tables_copy(s);
+    if (!e) e = launch_entropy_phase(s, nullptr);
+    if (!e) e = finish(s, f, flags);
+    hipStreamSynchronize(st);
+    *len = f.len;
+    return e;
 }
 
 }  // namespace jpge

@@ -16,6 +16,7 @@
 #include "host_io.hpp"
 #include "huffman.hpp"
 #include "kernels.hpp"
+#include "planes.hpp"
 
 namespace jpge {
 
@@ -55,6 +56,26 @@ class Encoder {
     // Stage entry: the four symbol histograms and first-occurrence keys.
     int symbol_stats(const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
                      uint32_t counts[1024], uint64_t first[1024]);
+
+    // ---- plane stages: the reference's Image stage methods on fp64 planes (planes.hip).
+    // Host or device buffers (kFlagDeviceInput / kFlagDeviceOutput); each call returns
+    // with its results in place.
+    // convertToColorSpace (Image.cpp:112-179): to_ycc 1 = RGB -> YCbCr, 0 = back
+    int stage_color(const double* const in[3], double* const out[3], size_t n, int to_ycc, uint32_t flags);
+    // Image::subsample with applySubsampling's mask for `mode` (jpge.h JPGE_S*)
+    static int subsample_shape(int mode, uint32_t rows, uint32_t cols, uint32_t* out_rows, uint32_t* out_cols);
+    int stage_subsample(const double* in, uint32_t rows, uint32_t cols, int mode, double* out, uint32_t flags);
+    // applyDCT(mode) (Image.cpp:540-595) over one plane of 8x8 blocks
+    int stage_dct(const double* in, uint32_t rows, uint32_t cols, int dct_mode, double* out, uint32_t flags);
+    // quantize (Coding.hpp:84-97) of every 8x8 block of a plane (applyQuantization)
+    int stage_quantize(const double* in, uint32_t rows, uint32_t cols, const uint8_t table[64], int32_t* out,
+                       uint32_t flags);
+    // writeJPEG (Image.cpp:831-976) on three fp64 planes of rows x cols (multiples of
+    // 16) in colour space `ycc` (0 RGB, 1 YCbCr with full-size chroma): convert,
+    // S420_m, Arai, quantise on the GPU, then the statistics and entropy kernels.
+    int encode_planes(const double* const planes[3], uint32_t rows, uint32_t cols, int ycc, uint32_t real_w,
+                      uint32_t real_h, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
+                      size_t* len, uint32_t flags);
 
     // ---- row stripes of a larger image (one stripe per device) ----
     // Phases, with the exchanges between them done by the caller (RCCL or a test):
@@ -143,6 +164,16 @@ class Encoder {
     void dump_stamps(const Slot& s);
     KernelTimes times_;
     std::mutex times_mu_;  // finish() of several lanes
+    // Serialises the context's public calls: single-frame calls share lane 0's first
+    // slot, and a batch uses every lane (jpge.h: a context is safe to share between
+    // threads; calls on it run one at a time).
+    std::recursive_mutex call_mu_;
+    // device scratch of the plane stages, grown on demand (index -> buffer)
+    std::vector<std::pair<void*, size_t>> scratch_;
+    void* scratch(int i, size_t bytes);
+  public:
+    std::recursive_mutex& call_mutex() { return call_mu_; }
+  private:
     std::mutex trace_mu_;
     std::vector<std::unique_ptr<Lane>> lanes_;  // JPGE_LANES (default 4: the device's hardware queues); lane 0 serves single-frame calls
 };
