@@ -287,9 +287,13 @@ static void color_conversion() {
     CHECK_CLOSE(rgb.R(1, 1), 0);
     CHECK_CLOSE(rgb.G(1, 1), 255);
     CHECK_CLOSE(rgb.B(1, 1), 119);
-    // and back: YCbCr -> RGB (Image.cpp:149-176)
+    // and back: YCbCr -> RGB, the reference's formula as written (Image.cpp:164-171: the
+    // chroma planes are offset by +128, not recentred; tests/test_gpu_planes.py pins
+    // the plane kernel to it bit for bit)
     auto back = ycc.convertToColorSpace(Image::RGB);
-    CHECK(std::fabs(back.B(1, 1) - 119) < 0.5 && std::fabs(back.G(1, 1) - 255) < 0.5);
+    const double y = ycc.Y(1, 1) + 128, cb = ycc.Cb(1, 1) + 128, cr = ycc.Cr(1, 1) + 128;
+    CHECK_EQUAL(back.G(1, 1), (1.f * y + -.344f * cb + -.714f * cr));
+    CHECK(back.colorSpace() == Image::RGB);
 }
 
 // ImageTest.cpp:75-199
