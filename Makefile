@@ -15,7 +15,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SR
 CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude
 
-HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp coding.cpp
+HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp coding.cpp group.cpp
 HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))
 DEV_SRCS  := fdct.hip stats.hip entropy.hip planes.hip
 DEV_OBJS  := $(addprefix $(BUILD)/,$(DEV_SRCS:.hip=.o))
@@ -39,7 +39,7 @@ $(BUILD)/%.o: $(SRC)/%.cpp $(HEADERS)
 
 $(LIBDIR)/libjpge.so: $(DEV_OBJS) $(HOST_OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $^ -L$(ROCM)/lib -lamdhip64
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $^ -L$(ROCM)/lib -lamdhip64 -ldl
 
 $(BINDIR)/jpgenc: $(SRC)/cli.cpp $(LIBDIR)/libjpge.so
 	@mkdir -p $(BINDIR)

@@ -334,6 +334,39 @@ int jpge_stripe_place(const jpge_stripe_summary* all, int n, int index, size_t h
 int jpge_stripe_pack(jpge_ctx* ctx, const jpge_stripe_summary* all, int n, int index, uint8_t* out, size_t cap,
                      size_t* seg_off, size_t* seg_len, size_t* total_len);
 
+/* ---- Device groups: one process, several devices ----
+ * A group owns one context per listed device and, when the devices are distinct, a
+ * single-process RCCL clique (ncclCommInitAll) over xGMI.  A device listed more than
+ * once (a rehearsal of N members on one GPU) makes the group exchange through host
+ * memory and device copies instead; the bytes are the same.  Replaces nothing in
+ * the reference (a single-threaded CPU encoder). */
+typedef struct jpge_group jpge_group;
+/* lanes: per member context, as jpge_open_ex.  JPGE_E_RCCL if librccl cannot be
+ * loaded or the communicators cannot be created. */
+int jpge_group_open(int ndev, const int* devices, int lanes, jpge_group** g);
+int jpge_group_close(jpge_group* g);
+/* members, and whether the exchanges ride RCCL (1) or host memory (0) */
+int jpge_group_size(const jpge_group* g, int* n, int* uses_rccl);
+/* member i's context (for per-member settings; owned by the group) */
+int jpge_group_context(jpge_group* g, int member, jpge_ctx** ctx);
+/* restart interval of every member (jpge_set_restart_interval) */
+int jpge_group_set_restart_interval(jpge_group* g, uint32_t mcus);
+/* Config 4: independent frames, frame i encoded by member i mod N (no collective);
+ * with JPGE_DEVICE_INPUT / _OUTPUT frame i's buffers live on that member's device.
+ * Per-frame len/status as jpge_encode_batch. */
+int jpge_group_encode_batch(jpge_group* g, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
+                            uint32_t flags);
+/* Config 5: one 4:2:0 image (host RGB8) in row stripes of whole MCU rows over the
+ * members — the jpge_stripe_* phases on every member at once, with an RCCL all-gather
+ * of the DC seeds, all-reduce of the histograms (sum) and first-occurrence keys
+ * (min), all-gather of the stripe summaries, and a grouped send/recv of the stuffed
+ * segments to member 0 — then the whole .jpg to host memory.  Byte-identical to
+ * jpge_encode_rgb8 on one device (with the group's restart interval, every stripe
+ * starts an interval and the DC seed exchange drops out). */
+int jpge_group_encode_striped(jpge_group* g, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
+                              int maxval, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
+                              size_t* len);
+
 #ifdef __cplusplus
 }
 #endif

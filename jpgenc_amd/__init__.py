@@ -43,6 +43,8 @@ EXPORTS = (
     "jpge_zigzag_index", "jpge_zigzag_block", "jpge_quantize_block", "jpge_rle_ac", "jpge_category_code",
     "jpge_encode_category", "jpge_dc_difference", "jpge_color_convert", "jpge_subsample_plane", "jpge_dct_plane",
     "jpge_quantize_plane", "jpge_encode_planes",
+    "jpge_group_open", "jpge_group_close", "jpge_group_size", "jpge_group_context", "jpge_group_set_restart_interval",
+    "jpge_group_encode_batch", "jpge_group_encode_striped",
 )
 
 JPGE_TO_RGB, JPGE_TO_YCBCR = 0, 1
@@ -163,6 +165,13 @@ def lib() -> ctypes.CDLL:
         L.jpge_quantize_plane.argtypes = [vp, vp, u32, u32, vp, vp, u32]
         L.jpge_encode_planes.argtypes = [vp, vp, vp, vp, u32, u32, i32, u32, u32, vp, vp, vp, sz, ctypes.POINTER(sz),
                                          u32]
+        L.jpge_group_open.argtypes = [i32, vp, i32, ctypes.POINTER(vp)]
+        L.jpge_group_close.argtypes = [vp]
+        L.jpge_group_size.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.jpge_group_context.argtypes = [vp, i32, ctypes.POINTER(vp)]
+        L.jpge_group_set_restart_interval.argtypes = [vp, u32]
+        L.jpge_group_encode_batch.argtypes = [vp, ctypes.POINTER(Frame), i32, vp, vp, u32]
+        L.jpge_group_encode_striped.argtypes = [vp, vp, u32, u32, sz, i32, vp, vp, vp, sz, ctypes.POINTER(sz)]
         _LIB = L
     return _LIB
 
@@ -603,6 +612,59 @@ class Encoder:
         _check(lib().jpge_symbol_stats(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(counts),
                                        _p(first), 0), "symbol_stats")
         return counts.reshape(4, 256), first.reshape(4, 256)
+
+
+class Group:
+    """A device group (jpge_group_open): one process, one context per listed device,
+    RCCL over xGMI between distinct devices (a device listed twice: host exchanges)."""
+
+    def __init__(self, devices, lanes: int = 0):
+        devs = (ctypes.c_int * len(devices))(*devices)
+        self._g = ctypes.c_void_p()
+        _check(lib().jpge_group_open(len(devices), devs, int(lanes), ctypes.byref(self._g)), "group_open")
+
+    def close(self) -> None:
+        if self._g:
+            lib().jpge_group_close(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def size(self) -> tuple[int, bool]:
+        """(members, whether the exchanges ride RCCL)"""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        _check(lib().jpge_group_size(self._g, ctypes.byref(n), ctypes.byref(r)), "group_size")
+        return n.value, bool(r.value)
+
+    def set_restart(self, mcus: int) -> None:
+        _check(lib().jpge_group_set_restart_interval(self._g, int(mcus)), "group_set_restart_interval")
+
+    def encode_batch(self, frames: list[np.ndarray], quality: int = 50, maxval: int = 255) -> list[bytes]:
+        """Config 4: frame i on member i mod N."""
+        qy, qc = quality_tables(quality)
+        frames = [np.ascontiguousarray(f, np.uint8) for f in frames]
+        outs = [np.empty(max_jpeg_bytes(f.shape[1], f.shape[0]), np.uint8) for f in frames]
+        arr = (Frame * len(frames))()
+        for i, (f, o) in enumerate(zip(frames, outs)):
+            arr[i].rgb, arr[i].width, arr[i].height = _p(f), f.shape[1], f.shape[0]
+            arr[i].stride, arr[i].maxval, arr[i].out, arr[i].cap = f.shape[1] * 3, maxval, _p(o), o.size
+        _check(lib().jpge_group_encode_batch(self._g, arr, len(frames), _p(qy), _p(qc), 0), "group_encode_batch")
+        return [outs[i][:arr[i].len].tobytes() for i in range(len(frames))]
+
+    def encode_striped(self, rgb: np.ndarray, quality: int = 50, maxval: int = 255) -> bytes:
+        """Config 5: one image in row stripes over the members."""
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        h, w = rgb.shape[:2]
+        qy, qc = quality_tables(quality)
+        out = np.empty(max_jpeg_bytes(w, h), np.uint8)
+        n = ctypes.c_size_t()
+        _check(lib().jpge_group_encode_striped(self._g, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(out),
+                                               out.size, ctypes.byref(n)), "group_encode_striped")
+        return out[:n.value].tobytes()
 
 
 def stripe_place(summaries: list, index: int, header_len: int) -> tuple[int, int]:
