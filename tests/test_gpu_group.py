@@ -33,7 +33,7 @@ def test_striped_group_matches_oracle(n, w, h, quality, kind):
         assert g.encode_striped(rgb, quality=quality) == _oracle.encode(rgb, quality)
 
 
-@pytest.mark.parametrize("n,restart", [(1, 120), (3, 120), (4, 37)])
+@pytest.mark.parametrize("n,restart", [(1, 120), (3, 120), (2, 37), (4, 60)])
 def test_striped_group_restart_matches_oracle(n, restart):
     rgb = J.synth_rgb8(9, 1920, 1080)
     with J.Group([0] * n, lanes=1) as g:
