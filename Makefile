@@ -6,12 +6,12 @@ ROCM     ?= /opt/rocm
 HIPCC    ?= $(ROCM)/bin/hipcc
 CXX      ?= g++
 ARCH     ?= gfx950
-BUILD    := build/obj
+BUILD    ?= build/obj
 SRC      := jpgenc_amd/csrc
-LIBDIR   := jpgenc_amd/lib
+LIBDIR   ?= jpgenc_amd/lib
 BINDIR   := jpgenc_amd/bin
 
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SRC) -Iinclude
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SRC) -Iinclude $(HIPEXTRA)
 CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude
 

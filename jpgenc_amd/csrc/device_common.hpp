@@ -40,6 +40,10 @@ namespace dev {
     } while (0)
 #endif
 
+// buffer-descriptor loads return 4 x u32 as a vector type
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 as_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
 // natural (row-major) index -> zig-zag position (inverse of Coding.hpp:57-81)
 static __constant__ uint8_t kNatToZz[64] = {
     0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42,
@@ -159,6 +163,15 @@ __device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, 
     return prevdc[pg - ((int64_t)b0 - 6)];
 }
 
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not
+// for its global loads or stores.  __syncthreads() is a workgroup fence as well,
+// whose s_waitcnt vmcnt(0) also waits for every prefetch in flight — a tile or
+// round loaded ahead would then arrive before the barrier passes and hide nothing.
+// Use only where the data other waves read after the barrier is in LDS.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Wait for this lane's outstanding global stores (so a following barrier publishes
 // them to the rest of the workgroup).
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -224,8 +237,9 @@ __device__ __forceinline__ void export_hist(const HistPtrs& h, uint32_t* host_cn
 }
 
 // block-wide exclusive scan of one value per thread (thread order); wsum holds
-// kWaves values of T
-template <int kWaves, typename T, typename W>
+// kWaves values of T.  kLdsSync: LDS-only barriers (lds_barrier), so global loads in
+// flight stay in flight.
+template <int kWaves, typename T, typename W, bool kLdsSync = false>
 __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total) {
     static_assert(sizeof(W) == 4 && (sizeof(T) == 4 || sizeof(T) == 8), "scan word types");
     T* ws = reinterpret_cast<T*>(wsum);
@@ -235,9 +249,11 @@ __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total
         const T o = __shfl_up(incl, d);
         if (lane >= d) incl += o;
     }
-    __syncthreads();
+    if (kLdsSync) lds_barrier();
+    else __syncthreads();
     if (lane == 63) ws[wv] = incl;
-    __syncthreads();
+    if (kLdsSync) lds_barrier();
+    else __syncthreads();
     T base = 0;
     total = 0;
 #pragma unroll

@@ -216,6 +216,9 @@ struct Encoder::Slot {
     uint8_t* d_ctl = nullptr;
     uint8_t* d_ubuf = nullptr;  // unstuffed entropy-coded segment (K3 internal)
     size_t cap_ubuf = 0;
+    uint32_t* d_recs = nullptr;    // K2's symbol records, kTileRecords per entropy tile
+    uint32_t* d_tcount = nullptr;  // records per tile
+    size_t cap_tiles = 0;
     uint8_t* d_out = nullptr;
     uint32_t* d_tab = nullptr;  // [1024] tables, then the header bytes (one upload)
     // pinned host staging
@@ -248,6 +251,7 @@ struct Encoder::Slot {
 
     ~Slot() {
         hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
+        hipFree(d_recs); hipFree(d_tcount);
         hipFree(d_out); hipFree(d_tab);
         hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_result);
         for (auto& e : ev) if (e) hipEventDestroy(e);
@@ -417,7 +421,7 @@ void Encoder::dump_stamps(const Slot& s) {
     if (!stamps_file_ || !d_dbg_) return;
     std::vector<uint64_t> h(dbg_words_);
     if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(s.g), layout(s.g).grid(),
+    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(layout(s.g)), layout(s.g).grid(),
                              layout(s.g).grid()};
     FILE* f = std::fopen(stamps_file_, "wb");
     if (!f) return;
@@ -436,6 +440,14 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         s.cap_blk = nblk;
     }
     const CtlLayout L(layout(g).grid());
+    const size_t ntiles = seg_tiles(layout(g));
+    if (ntiles > s.cap_tiles) {
+        hipFree(s.d_recs); hipFree(s.d_tcount);
+        s.d_recs = nullptr; s.d_tcount = nullptr; s.cap_tiles = 0;
+        JPGE_HIP(hipMalloc((void**)&s.d_recs, ntiles * kTileRecords * 4));
+        JPGE_HIP(hipMalloc((void**)&s.d_tcount, ntiles * 4));
+        s.cap_tiles = ntiles;
+    }
     const size_t ubuf = entropy_ubuf_bytes(layout(g));
     if (ubuf > s.cap_ubuf) {
         hipFree(s.d_ubuf); s.d_ubuf = nullptr; s.cap_ubuf = 0;
@@ -495,6 +507,9 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.key_y0 = s.key_y0;
     st.key_c0 = s.key_c0;
     st.key_ncb = s.key_ncb;
+    st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs_);
+    st.recs = s.d_recs;
+    st.tcount = s.d_tcount;
     st.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
     return st;
 }
@@ -503,6 +518,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     const CtlLayout L(layout(s.g).grid());
     EntropyArgs e;
     e.coef = s.d_coef;
+    e.recs = s.d_recs;
+    e.tcount = s.d_tcount;
     e.g = s.g;
     e.tables = s.d_tab;
     e.out = s.out_dev;

@@ -4,11 +4,12 @@
 //
 // entropy_code_kernel — G persistent workgroups; workgroup w owns the contiguous
 //   tiles [w*T/G, (w+1)*T/G) of 128 blocks (2..kEntropyMaxTilesPerWg tiles).
-//   Per tile (the next tile loads into registers meanwhile): stage, each lane
-//   emits its part (DC / 16 zig-zag positions / EOB) once into a private LDS slot,
-//   tile scan of the part lengths, compaction into a big-endian word stage at the
-//   workgroup-LOCAL bit offset, complete words to the workgroup's private region R
-//   (the partial last word carries into the next tile).  Then the workgroup counts
+//   Per tile: its symbol records (written by the statistics kernel, stream order)
+//   in rounds of 4 per thread — code bits from the tables, a workgroup scan of the
+//   bit counts, each record ORed into a big-endian word stage at its workgroup-LOCAL
+//   bit offset (the next round's records load meanwhile) — then complete words to
+//   the workgroup's private region R (the partial last word carries into the next
+//   tile).  Then the workgroup counts
 //   the 0xFF bytes its stream would hold at each of the 8 byte alignments and
 //   writes a record {bits, first 8 bits, last 8 bits, ff[8]}.
 // entropy_pack_kernel — G workgroups; each scans all G records (L2-resident): bit
@@ -19,14 +20,20 @@
 //   belongs to the workgroup holding its last bit; the last one 1-fills and writes
 //   EOI.  No workgroup ever waits for another: the kernel boundary is the only
 //   synchronisation.
-// Global traffic: the coefficients once (HBM); R written once, read twice (L2 /
-// Infinity Cache, workgroup-private lines); the records; the output once.
+// Global traffic: the symbol records once; R written once, read twice (L2 /
+// Infinity Cache, workgroup-private lines); the workgroup records; the output once.
 #include "device_common.hpp"
 
 namespace jpge {
 namespace {
 using namespace dev;
 
+#ifndef K3_ZERO_TILE
+#define K3_ZERO_TILE 0
+#endif
+#ifndef K3_PACK_BRANCHY
+#define K3_PACK_BRANCHY 1  // (measured: the branch-free 64-bit form ran 6 us slower per 4K frame)
+#endif
 constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
@@ -36,9 +43,6 @@ constexpr int kWin = 32;                                              // output 
 constexpr int kWinWords = kWin / 4;
 static_assert(kWinWords == 8 && kEntropyRegionBytes % 16 == 0, "pack loads a window as two aligned uint4");
 constexpr int kChunk = kK3Threads * kWin;                             // output bytes per round (pre-stuffing)
-// One part's bits: DC <= 16+11, 16 AC symbols <= 16+11 each, <= 3 ZRL (a part
-// spans 16 positions, so only its first run can reach 16), EOB <= 16 -> < 512.
-constexpr int kSlotWords = 16;
 
 // per-workgroup record handed from the code kernel to the pack kernel
 struct alignas(16) WgRecord {
@@ -51,42 +55,12 @@ constexpr int kRecBits = 8, kRecEdge = 9;  // u32 indices
 static_assert(sizeof(WgRecord) == kEntropyRecordBytes, "record size");
 
 struct K3Lds {
-    union {
-        int16_t zz[kK3Blocks * kZzStride];  // staged tile (coding pass)
-        uint32_t stage[kStageWords];        // the tile's big-endian bit stream (compaction, store)
-    } u;
-    uint32_t slot[kSlotWords * kK3Threads];  // every lane's part, MSB first; word k at [k][tid]
-    uint32_t tab[4 * 256];                   // (len << 16) | code
-    uint64_t bmask[kK3Blocks];
-    int prevdc[6];
-    uint32_t sbits[kK3Threads];  // bits of every part, stream order; then their offsets
+    uint32_t stage[kStageWords];  // the tile's big-endian bit stream
+    uint32_t tab[4 * 256];        // (len << 16) | code
+    uint32_t tcnt[kMaxTiles];     // symbol records of each of the workgroup's tiles
     uint32_t wsum[kK3Waves];
     uint32_t cnt8[8];
     uint32_t carry;
-};
-
-// MSB-first bit sink over one lane's private LDS slot (word k at s[k * stride]).
-// Branch-free: the current word is stored on every put (a partial word is simply
-// rewritten until it completes).
-struct SlotSink {
-    uint32_t* s;
-    uint32_t k;     // index of the current word
-    uint32_t cur;   // current word, MSB-aligned
-    uint32_t fill;  // bits in cur, 0..31
-    __device__ __forceinline__ void init(uint32_t* slot) { s = slot; k = 0; cur = 0; fill = 0; }
-    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {  // 0 <= n <= 32, v < 2^n
-        const uint32_t t = fill + n;                                  // <= 63
-        const uint32_t out = cur | (uint32_t)(((uint64_t)v << 32) >> t);
-        s[k * kK3Threads] = out;
-        const bool full = t >= 32;
-        cur = full ? (uint32_t)((uint64_t)v << (64 - t)) : out;
-        fill = full ? t - 32 : t;
-        k += full ? 1u : 0u;
-    }
-    __device__ __forceinline__ uint32_t finish() {  // total bits
-        if (fill) s[k * kK3Threads] = cur;           // spill bits of a word-completing last put
-        return 32 * k + fill;
-    }
 };
 
 // 0x80 in every byte of the big-endian word y that is 0xFF
@@ -101,58 +75,14 @@ __device__ __forceinline__ uint32_t byte_range(int lo, int hi) {
     return ge & lt & 0x80808080u;
 }
 
-// One lane's part of a block: DC (part 0), the run/size symbols of its 16 zig-zag
-// positions, EOB (part 3) — doHuffmanEncoding, Image.cpp:737-829.
-struct PartCoder {
-    PartView pv;
-    const uint32_t* tdc;
-    const uint32_t* tac;
-    uint64_t mask;
-    int part, dcdiff;
-    bool active;
-};
-
-__device__ __forceinline__ PartCoder make_coder(const K3Lds& L, uint64_t b0, int nb, int blk, int part,
-                                                const DcSeed& seed, const Restart& rs, uint32_t bpm) {
-    PartCoder c;
-    c.part = part;
-    c.active = blk < nb;
-    const bool chroma = block_comp((int)((b0 + blk) % bpm), bpm) != 0;
-    c.tdc = &L.tab[(chroma ? 2 : 0) * 256];
-    c.tac = &L.tab[(chroma ? 3 : 1) * 256];
-    c.mask = c.active ? L.bmask[blk] : 0ull;
-    c.pv.load(L.u.zz, c.mask, blk, part, c.active);
-    // DC difference to the chain predecessor, Image.cpp:638-678
-    c.dcdiff =
-        (c.active && part == 0) ? L.u.zz[blk * kZzStride] - pred_dc(b0, blk, L.u.zz, L.prevdc, seed, rs, bpm) : 0;
-    return c;
-}
-
-// Emit the part into the lane's slot in stream order; returns its bit count.
-__device__ __forceinline__ uint32_t code_part(const PartCoder& c, SlotSink& bs) {
-    if (c.active && c.part == 0) {
-        const int dcat = category(c.dcdiff);
-        const uint32_t ent = c.tdc[dcat];
-        const uint32_t db = (uint32_t)(c.dcdiff < 0 ? c.dcdiff + (1 << dcat) - 1 : c.dcdiff) & ((1u << dcat) - 1);
-        bs.put(((ent & 0xFFFF) << dcat) | db, (ent >> 16) + dcat);
-    }
-    const uint32_t zrl = c.tac[0xF0];
-    for_each_ac(c.pv, c.part, [&](int p, int run, int v) {
-        const uint32_t av = (uint32_t)(v < 0 ? -v : v);
-        __builtin_assume(av != 0);
-        const uint32_t cat = 32 - __builtin_clz(av);
-        if (run >= 16) {  // rare: up to 3 ZRL codes
-            for (; run >= 16; run -= 16) bs.put(zrl & 0xFFFF, zrl >> 16);
-        }
-        const uint32_t ent = c.tac[(run << 4) | cat];
-        const uint32_t vb = (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1);  // v - 1 when negative
-        bs.put(((ent & 0xFFFF) << cat) | vb, (ent >> 16) + cat);
-    });
-    if (c.active && c.part == 3 && !(c.mask >> 63)) {  // EOB
-        const uint32_t ent = c.tac[0];
-        bs.put(ent & 0xFFFF, ent >> 16);
-    }
-    return bs.finish();
+// One symbol record (K2, kernels.hpp) as code bits: the table's code, then the
+// extra bits (the category's count of them); returns the bit count (<= 16 + 15).
+__device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, uint32_t& bits) {
+    const uint32_t sym = (r >> 16) & 0xFF, t = r >> 24;
+    const uint32_t nb = (t & 1) ? (sym & 15) : sym;  // AC: the symbol's size; DC: its category
+    const uint32_t ent = tab[(t << 8) | sym];
+    bits = ((ent & 0xFFFF) << nb) | (r & 0xFFFF);
+    return (ent >> 16) + nb;
 }
 
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_code_kernel(
@@ -169,15 +99,14 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
     const int ntl = (int)wt.nt;
+    if (tid < ntl) L.tcnt[tid] = a.tcount[wt.seg * a.seg.tps + wt.t0 + tid];
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
-    auto tile_b0 = [&](int lt) { return wt.tile_b0(wt.t0 + lt); };
-    auto tile_nb = [&](int lt) { return (int)wt.tile_nb(wt.t0 + lt); };
 
     // ---- emit every tile at workgroup-local bit offsets into R ----
-    TileRegs<kK3Threads, kK3Blocks> regs;
-    regs.init(tid);
-    regs.load(a.coef, tile_b0(0), tile_nb(0), tid);
+    // The tile's symbol records (K2) in rounds of 4 per thread: code bits of each,
+    // a workgroup scan of the thread totals, each thread's records ORed into the
+    // stage at its offset (every record spans at most two words).
     uint32_t wl = 0;  // workgroup-local bit position of the current tile
     // 0xFF bytes of the stream at each byte alignment, counted on the stage words as
     // they are stored (see the note after the loop).  A word's count needs the next
@@ -194,64 +123,108 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     uint32_t pend = 0;
     bool has_pend = false;
     uint64_t tq = JPGE_NOW();
+    // Records through a buffer descriptor over this workgroup's tiles: every round
+    // issues its next load unconditionally (past the end: an out-of-range offset,
+    // zeros), so no branch merges in-flight registers and the in-order wait for a
+    // round's records never waits for the prefetch behind it.
+    const uint32_t gt0 = wt.seg * a.seg.tps + wt.t0;  // global number of the first tile
+    const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * kTileRecords * 4, 0x00020000);
+    constexpr uint32_t kRound = 4 * kK3Threads;  // records per round
+    auto rec_load = [&](uint32_t off_rec) -> uint4 {  // off_rec: uniform record offset, ~0u = none
+        const uint32_t off = off_rec == ~0u ? 0xFFFFFFF0u : (off_rec + 4 * tid) * 4;
+        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rec_rs, off, 0, 0));
+    };
+    uint4 nxt = rec_load(0);
     for (int lt = 0; lt < ntl; ++lt) {
-        const uint64_t b0 = tile_b0(lt);
-        const int nb = tile_nb(lt);
-        __syncthreads();  // previous tile: stage stored, carry set (u is free); tables loaded
-        regs.stage(nb, L.u.zz, L.bmask, L.prevdc, tid);
-        if (lt + 1 < ntl) regs.load(a.coef, tile_b0(lt + 1), tile_nb(lt + 1), tid);
-        __syncthreads();
+        // previous tile: stage stored, carry set; tables and tile counts in LDS
+        // (LDS-only barrier: the records in flight stay in flight)
+        lds_barrier();
         JPGE_ACC(0, tq);
-        uint32_t n;  // bits of this lane's part
-        {
-            const PartCoder pc = make_coder(L, b0, nb, blk, part, a.seed, a.rst, a.g.bpm);
-            SlotSink ss;
-            ss.init(L.slot + tid);
-            n = code_part(pc, ss);
-        }
-        L.sbits[blk * 4 + part] = n;
-        __syncthreads();
-        JPGE_ACC(1, tq);
-        uint32_t T;  // scan in stream order (thread tid takes stream index tid)
-        const uint32_t ex = block_scan<kK3Waves>(L.sbits[tid], L.wsum, lane, wv, T);
-        L.sbits[tid] = ex;
+        const uint32_t nrec = __builtin_amdgcn_readfirstlane(L.tcnt[lt]);
         const uint32_t lead = wl & 31;
-        const uint32_t ncw = (lead + T) >> 5;  // complete words of the tile stream
-        for (uint32_t i = tid; i <= ncw; i += kK3Threads) L.u.stage[i] = 0;  // (zz is dead)
-        __syncthreads();
-        JPGE_ACC(2, tq);
-        // compaction: OR the part's slot words into the stage at its stream offset
-        {
-            const uint32_t pos0 = lead + L.sbits[blk * 4 + part];
-            for (uint32_t k = 0; 32 * k < n; ++k) {
-                const uint32_t v = L.slot[k * kK3Threads + tid];
-                const uint32_t pos = pos0 + 32 * k, sh = pos & 31, len = min(32u, n - 32 * k);
-                atomicOr(&L.u.stage[pos >> 5], v >> sh);
-                if (sh + len > 32) atomicOr(&L.u.stage[(pos >> 5) + 1], v << (32 - sh));
+        uint32_t pos = lead;  // bit position in the stage
+#if K3_ZERO_TILE
+        // the whole stage zeroed once per tile (no per-round zeroing barrier)
+        for (uint32_t w = tid; w < kStageWords / 4; w += kK3Threads)
+            reinterpret_cast<uint4*>(L.stage)[w] = make_uint4(0, 0, 0, 0);
+        lds_barrier();
+#else
+        if (tid == 0) L.stage[0] = 0;
+#endif
+        for (uint32_t r0 = 0; r0 < nrec; r0 += kRound) {
+            const uint4 rv = nxt;
+            // prefetch: the next round of this tile, else the next tile's first round
+            const uint32_t nofs = r0 + kRound < nrec ? lt * kTileRecords + r0 + kRound
+                                  : lt + 1 < ntl      ? (lt + 1) * kTileRecords
+                                                      : ~0u;
+            nxt = rec_load(nofs);
+            const uint32_t i0 = r0 + 4 * tid;
+            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+            uint32_t cb[4], cl[4], tl = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t n = rec_bits(rr[q], L.tab, cb[q]);
+                cl[q] = i0 + q < nrec ? n : 0u;
+                tl += cl[q];
             }
+            JPGE_ACC(3, tq);
+            uint32_t T;
+            const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true>(tl, L.wsum, lane, wv, T);
+            JPGE_ACC(4, tq);
+#if !K3_ZERO_TILE
+            // zero the stage words this round reaches past the current partial word
+            for (uint32_t w = (pos >> 5) + 1 + tid; w <= ((pos + T) >> 5); w += kK3Threads) L.stage[w] = 0;
+            lds_barrier();
+#endif
+            JPGE_ACC(5, tq);
+            // each record into the one or two stage words it spans
+            uint32_t bp = pos + ex;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#if K3_PACK_BRANCHY
+                if (cl[q]) {
+                    const uint32_t sh = bp & 31, n = cl[q];
+                    const uint32_t v = cb[q] << (32 - n);  // MSB-aligned (n >= 1)
+                    atomicOr(&L.stage[bp >> 5], v >> sh);
+                    if (sh + n > 32) atomicOr(&L.stage[(bp >> 5) + 1], v << (32 - sh));
+                    bp += n;
+                }
+#else
+                const uint32_t n = cl[q], sh = bp & 31;
+                const uint64_t v = n ? ((uint64_t)cb[q] << (64 - n)) >> sh : 0ull;  // MSB-aligned at bp
+                atomicOr(&L.stage[bp >> 5], (uint32_t)(v >> 32));
+                if ((uint32_t)v) atomicOr(&L.stage[(bp >> 5) + 1], (uint32_t)v);
+                bp += n;
+#endif
+            }
+            pos += T;
+            lds_barrier();
+            JPGE_ACC(6, tq);
         }
-        __syncthreads();
-        JPGE_ACC(3, tq);
+        const uint32_t T = pos - lead;  // this tile's bits
+        const uint32_t ncw = pos >> 5;  // complete words of the tile stream
+        JPGE_ACC(1, tq);
         const uint32_t wbase = wl >> 5;
         for (uint32_t w = tid; w < ncw; w += kK3Threads) {
-            uint32_t v = L.u.stage[w];
+            uint32_t v = L.stage[w];
             if (w == 0) v |= L.carry;  // partial last word of the previous tile
             R32[wbase + w] = __builtin_bswap32(v);
-            if (w + 1 < ncw) count_word(v, L.u.stage[w + 1]);
+            if (w + 1 < ncw) count_word(v, L.stage[w + 1]);
         }
         if (tid == 0) {  // (thread 0 consumed the old carry above)
             if (ncw) {
-                const uint32_t w0 = L.u.stage[0] | L.carry;
+                const uint32_t w0 = L.stage[0] | L.carry;
                 if (has_pend) count_word(pend, w0);
-                pend = ncw == 1 ? w0 : L.u.stage[ncw - 1];
+                pend = ncw == 1 ? w0 : L.stage[ncw - 1];
                 has_pend = true;
             }
-            uint32_t v = L.u.stage[ncw];
+            uint32_t v = L.stage[ncw];
             if (ncw == 0) v |= L.carry;
             L.carry = v;
         }
         wl += T;
-        JPGE_ACC(4, tq);
+        JPGE_ACC(2, tq);
     }
     const uint32_t Lb = wl;  // this workgroup's bits (>= 6: every block codes >= 2 bits, >= 3 blocks)
     if (tid == 0 && (Lb & 31)) R32[Lb >> 5] = __builtin_bswap32(L.carry);
@@ -687,7 +660,7 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
         const uint32_t nt = (nb + kK3Blocks - 1) / kK3Blocks;
         uint32_t G = 1;
         if (nt > 1) {
-            const uint32_t lo = (nt + kMaxTiles - 1) / kMaxTiles, hi = nt / 2;
+            const uint32_t lo = (nt + kMaxTiles - 1) / kMaxTiles, hi = nt;
             G = want < lo ? lo : (want > hi ? hi : want);
         }
         L.nseg = 1;

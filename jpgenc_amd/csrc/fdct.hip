@@ -48,8 +48,6 @@ __device__ __forceinline__ int quant_fast(double w, double c, bool& near_half) {
 
 __device__ __forceinline__ int quant_exact(double w, double s, double q) { return (int)round((w * s) / q); }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 as_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's range
 #ifndef K1_STORE_AUX
 #define K1_STORE_AUX 16  // sc1: write-through coefficient stores (no dirty L2 lines at the kernel's end)

@@ -134,6 +134,17 @@ JPGE_HD inline WgTiles wg_tiles(const SegLayout& L, uint32_t w) {
     return r;
 }
 
+// Symbol records (K2 -> K3): the entropy-coded symbols of a tile in stream order,
+// one u32 each: table << 24 | symbol << 16 | extra bits (table 0 Y-DC, 1 Y-AC,
+// 2 C-DC, 3 C-AC; the extra bits' count is the symbol's category: symbol & 15 for
+// AC, the symbol itself for DC).  A block codes at most 64 symbols (DC + 63 AC, or
+// DC + 62 AC + EOB; a zero run long enough for a ZRL removes a coefficient), so a
+// tile's records fit kTileRecords words; tile t's sit at recs + t * kTileRecords,
+// its count at tcount[t].  Tiles are the entropy partition's (seg_layout), numbered
+// segment by segment.
+constexpr int kRecPerBlock = 64;
+constexpr int kTileRecords = kEntropyTile * kRecPerBlock;
+
 struct StatsArgs {
     const int16_t* coef;
     Geometry g;
@@ -144,6 +155,9 @@ struct StatsArgs {
     // Y raster index of the stripe's first Y block, Cb raster index of its first
     // Cb block, and the image's Cb block count (every Cr key follows all Cb keys)
     uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
+    SegLayout seg;       // the entropy partition: the tiles the records are written in
+    uint32_t* recs;      // [tiles][kTileRecords] symbol records
+    uint32_t* tcount;    // [tiles] records per tile
     uint64_t* dbg;
 };
 
@@ -175,6 +189,8 @@ constexpr uint32_t kExtPlace = 4u;     // pack kernel reads WgPlace (entropy_sca
 
 struct EntropyArgs {
     const int16_t* coef;
+    const uint32_t* recs;    // the statistics kernel's symbol records (kTileRecords per tile)
+    const uint32_t* tcount;  // records per tile
     Geometry g;
     const uint32_t* tables;  // [4][256] (len << 16) | code, followed by the header bytes
     uint8_t* out;            // whole .jpg; the kernel writes the header to [0, hdr_len)
@@ -210,6 +226,20 @@ struct EntropyArgs {
     uint64_t* dbg;
 };
 
+// tiles of a partition, and tile gt's blocks (the global tile number of segment s's
+// tile i is s * tps + i)
+JPGE_HD inline uint32_t seg_tiles(const SegLayout& L) { return (L.nseg - 1) * L.tps + L.ltps; }
+JPGE_HD inline void seg_tile(const SegLayout& L, uint32_t gt, uint64_t& b0, uint32_t& nb) {
+    uint32_t seg, i, tps, nbs;
+    if (gt < (L.nseg - 1) * L.tps) {
+        seg = gt / L.tps; i = gt % L.tps; tps = L.tps; nbs = L.sblk;
+    } else {
+        seg = L.nseg - 1; i = gt - seg * L.tps; tps = L.ltps; nbs = L.lblk;
+    }
+    b0 = (uint64_t)seg * L.sblk + (uint64_t)i * nbs / tps;
+    nb = (uint32_t)((uint64_t)(i + 1) * nbs / tps - (uint64_t)i * nbs / tps);
+}
+
 inline uint32_t entropy_tiles(const Geometry& g) {
     return (g.nblocks() + kEntropyTile - 1) / kEntropyTile;
 }
@@ -218,7 +248,7 @@ inline uint32_t entropy_tiles(const Geometry& g) {
 constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntropyTile * kStageBytesPerBlock + 128;
 
 uint32_t fdct_grid(const Geometry& g, bool solo);
-uint32_t stats_grid(const Geometry& g);
+uint32_t stats_grid(const SegLayout& L);
 // entropy partition of a frame: restart_mcus = 0 -> one segment over 128-block tiles
 // (2..kEntropyMaxTilesPerWg per workgroup, about 512 workgroups or wgs_override)
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override);

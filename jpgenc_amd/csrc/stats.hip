@@ -1,6 +1,9 @@
 // K2 stats_kernel (gfx950): DC difference chain (Image.cpp:638-678) + zig-zag RLE
 // + category coding (Coding.hpp:148-283) -> the four symbol histograms of
-// writeJPEG's "texts" (Image.cpp:888-906) with first-occurrence keys.
+// writeJPEG's "texts" (Image.cpp:888-906) with first-occurrence keys, and the
+// symbol records of every tile in stream order (kernels.hpp), which the entropy
+// code kernel turns into bits once the tables exist: the run-length and category
+// work is done once per frame.
 //
 // Lane mapping: PartView (device_common.hpp), four lanes per block, one wave per
 // 16 zig-zag positions of 64 blocks.  Persistent grid:
@@ -37,13 +40,22 @@ struct K2Lds {
     uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
     uint64_t bmask[kK2Blocks];
     int prevdc[6];
+    uint32_t pcnt[kK2Threads];           // records of every part (stream order), then their offsets
+    uint32_t wsum[kK2Threads / 64];
+    uint32_t recs[kTileRecords];         // the tile's symbol records, stream order
 };
+
+// Record words (kernels.hpp): table << 24 | symbol << 16 | extra bits.
+__device__ __forceinline__ uint32_t rec_word(uint32_t table, uint32_t sym, uint32_t bits) {
+    return (table << 24) | (sym << 16) | bits;
+}
 
 __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     __shared__ K2Lds lds;
     const int tid = threadIdx.x;
-    const uint32_t nblocks = a.g.nblocks(), mw = a.g.mw;
-    const uint32_t ntiles = (nblocks + kK2Blocks - 1) / kK2Blocks;
+    const uint32_t mw = a.g.mw;
+    // the entropy partition's tiles (seg_layout), a contiguous run per workgroup
+    const uint32_t ntiles = seg_tiles(a.seg);
     const uint32_t t_first = (uint32_t)((uint64_t)blockIdx.x * ntiles / gridDim.x);
     const uint32_t t_last = (uint32_t)((uint64_t)(blockIdx.x + 1) * ntiles / gridDim.x);
     for (int i = tid; i < kHistCopies * kCopyWords; i += kK2Threads) (&lds.acnt[0][0])[i] = 0;
@@ -55,24 +67,33 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     const uint32_t bpm = a.g.bpm, yh = a.g.yh, yv = a.g.yv();  // MCU = yh x yv Y blocks + Cb + Cr
     const uint64_t ybw = (uint64_t)mw * yh;                    // Y blocks per block row
     const uint32_t yhs = (uint32_t)__builtin_ctz(yh);          // yh is 1, 2 or 4: k / yh = k >> yhs
-    const uint32_t mrow0 = (uint32_t)(((uint64_t)t_first * kK2Blocks) / bpm) / mw;
+    uint64_t fb0 = 0;
+    uint32_t fnb = 0;
+    if (t_first < t_last) seg_tile(a.seg, t_first, fb0, fnb);
+    const uint32_t mrow0 = (uint32_t)(fb0 / bpm) / mw;
     const uint64_t ybase = (uint64_t)mrow0 * yv * ybw;
     const uint64_t cbase = (uint64_t)mrow0 * mw;
     const int lane = tid & 63, wv = tid >> 6;
     const int blk = block_of(wv, lane), part = part_of(wv);
-    auto tile_nb = [&](uint32_t t) { return (int)min((uint64_t)kK2Blocks, nblocks - (uint64_t)t * kK2Blocks); };
     TileRegs<kK2Threads, kK2Blocks> regs;
     regs.init(tid);
-    if (t_first < t_last) regs.load(a.coef, (uint64_t)t_first * kK2Blocks, tile_nb(t_first), tid);
+    if (t_first < t_last) regs.load(a.coef, fb0, (int)fnb, tid);
 
     uint64_t tq = JPGE_NOW();
     for (uint32_t tile = t_first; tile < t_last; ++tile) {
-        const uint64_t b0 = (uint64_t)tile * kK2Blocks;
-        const int nb = tile_nb(tile);
-        __syncthreads();  // previous tile's readers are done with zz / bmask
+        uint64_t b0;
+        uint32_t nbu;
+        seg_tile(a.seg, tile, b0, nbu);
+        const int nb = (int)nbu;
+        lds_barrier();  // previous tile's readers are done with zz / bmask / recs
         regs.stage(nb, lds.zz, lds.bmask, lds.prevdc, tid);
-        if (tile + 1 < t_last) regs.load(a.coef, b0 + kK2Blocks, tile_nb(tile + 1), tid);
-        __syncthreads();
+        if (tile + 1 < t_last) {  // (stays in flight across the LDS-only barriers below)
+            uint64_t nb0;
+            uint32_t nnb;
+            seg_tile(a.seg, tile + 1, nb0, nnb);
+            regs.load(a.coef, nb0, (int)nnb, tid);
+        }
+        lds_barrier();
         JPGE_STAMP(1);
         JPGE_ACC(0, tq);
         const bool active = blk < nb;
@@ -95,30 +116,65 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         const uint64_t mask = lds.bmask[blk];
         PartView pv;
         pv.load(lds.zz, mask, blk, part, active);
+        const bool eob = active && part == 3 && !(mask >> 63);
+        // this part's records: DC, its ZRLs (only the first run of a 16-position part
+        // can reach 16) and run/size symbols, EOB — then its offset in the tile's stream
+        {
+            uint32_t n = 0;
+            if (active) {
+                n = (part == 0 ? 1u : 0u) + (uint32_t)__builtin_popcount(pv.m16) + (eob ? 1u : 0u);
+                if (pv.m16) n += (uint32_t)(16 * part + __builtin_ctz(pv.m16) - pv.last - 1) >> 4;
+            }
+            lds.pcnt[blk * 4 + part] = n;
+        }
+        lds_barrier();
+        uint32_t T;  // the tile's records
+        const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(lds.pcnt[tid], lds.wsum, lane, wv, T);
+        lds.pcnt[tid] = ex;
+        lds_barrier();
+        JPGE_ACC(1, tq);
+        uint32_t o = lds.pcnt[blk * 4 + part];
         if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
-            const int dcat = category(lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst, bpm));
+            const int dd = lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst, bpm);
+            const int dcat = category(dd);
             atomicAdd(&lds.dcnt[lane & (kHistCopies - 1)][tsel * 16 + dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
+            const uint32_t db = (uint32_t)(dd < 0 ? dd + (1 << dcat) - 1 : dd) & ((1u << dcat) - 1);
+            lds.recs[o++] = rec_word(2 * tsel, (uint32_t)dcat, db);
         }
         const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
         uint32_t* cnt = &lds.acnt[lane & (kHistCopies - 1)][tsel * 256];
         uint32_t* key = lds.key[2 * tsel + 1];
+        const uint32_t tac = 2 * tsel + 1;
         for_each_ac(pv, part, [&](int p, int run, int v) {
-            const int sym = ((run & 15) << 4) | category(v);
+            const int cat = category(v);
+            const int sym = ((run & 15) << 4) | cat;
             atomicAdd(&cnt[sym], 1u);
             const uint32_t kk = acb + 2u * p + 1u;
             if (kk < key[sym]) atomicMin(&key[sym], kk);
             if (run >= 16) {
                 atomicAdd(&cnt[0xF0], (uint32_t)(run >> 4));
                 if (kk - 1u < key[0xF0]) atomicMin(&key[0xF0], kk - 1u);
+                for (int r = run; r >= 16; r -= 16) lds.recs[o++] = rec_word(tac, 0xF0, 0);
             }
+            lds.recs[o++] = rec_word(tac, (uint32_t)sym, (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1));
         });
-        if (active && part == 3 && !(mask >> 63)) {  // EOB
+        if (eob) {
             atomicAdd(&cnt[0], 1u);
             if (acb + 127u < key[0]) atomicMin(&key[0], acb + 127u);
+            lds.recs[o] = rec_word(tac, 0, 0);
         }
-        JPGE_ACC(1, tq);
+        lds_barrier();
+        JPGE_ACC(2, tq);
+        // the tile's records to HBM, coalesced (16 bytes per lane)
+        {
+            uint4* dst = reinterpret_cast<uint4*>(a.recs + (uint64_t)tile * kTileRecords);
+            const uint4* src = reinterpret_cast<const uint4*>(lds.recs);
+            for (uint32_t i = tid; 4 * i < T; i += kK2Threads) dst[i] = src[i];
+            if (tid == 0) a.tcount[tile] = T;
+        }
+        JPGE_ACC(3, tq);
     }
     __syncthreads();
     JPGE_STAMP(2);
@@ -171,13 +227,13 @@ hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* h
     return hipGetLastError();
 }
 
-uint32_t stats_grid(const Geometry& g) {
-    const uint32_t tiles = (g.nblocks() + kK2Blocks - 1) / kK2Blocks;
+uint32_t stats_grid(const SegLayout& L) {
+    const uint32_t tiles = seg_tiles(L);
     return tiles < 512 ? tiles : 512;  // 2 per CU, persistent over contiguous tiles
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(stats_kernel, dim3(stats_grid(a.g)), dim3(kK2Threads), 0, s, a);
+    hipLaunchKernelGGL(stats_kernel, dim3(stats_grid(a.seg)), dim3(kK2Threads), 0, s, a);
     return hipGetLastError();
 }
 

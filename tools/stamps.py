@@ -15,8 +15,8 @@ PHASES = {
     "entropy_pack": ["start", "scan", "output", "", "", "", "", ""],
 }
 ACC = {
-    "stats": ["stage", "count"],
-    "entropy_code": ["stage", "code", "scan", "compact", "store"],
+    "stats": ["stage", "count+scan", "symbols", "store"],
+    "entropy_code": ["sync", "rounds(tail)", "store", "load+bits", "scan", "zero", "pack"],
 }
 
 
