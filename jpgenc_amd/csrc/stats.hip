@@ -33,26 +33,62 @@ constexpr int kCopyWords = 2 * 256 + 4;
 // and bank stagger (stride 36 words) split them.
 constexpr int kDcCopyWords = 2 * 16 + 4;
 
+constexpr int kMaxNz = kK2Blocks * 63;  // AC non-zeros of a tile, at most
+constexpr int kK2MaxRun = 256;           // tiles per workgroup, at most (stats_grid)
+
+// x / d and x % d for x < 2^24 (float reciprocal, corrected): the index arithmetic
+// stays in 32-bit registers (a 64-bit division costs ~100 instructions per lane)
+__device__ __forceinline__ uint32_t udiv24(uint32_t x, uint32_t d, float inv, uint32_t& r) {
+    uint32_t q = (uint32_t)((float)x * inv);
+    int32_t rr = (int32_t)(x - q * d);
+    if (rr < 0) { --q; rr += (int32_t)d; }
+    if (rr >= (int32_t)d) { ++q; rr -= (int32_t)d; }
+    r = (uint32_t)rr;
+    return q;
+}
+
 struct K2Lds {
-    int16_t zz[kK2Blocks * kZzStride];
+    uint32_t nz[kMaxNz];                 // the tile's AC non-zeros in stream order: v & 0xFFFF | p << 16 | blk << 22
     uint32_t acnt[kHistCopies][kCopyWords];  // AC counters (Y-AC at 0, C-AC at 256), per copy
     uint32_t dcnt[kHistCopies][kDcCopyWords];  // DC counters (Y-DC at 0, C-DC at 16), per copy
     uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
-    uint64_t bmask[kK2Blocks];
+    uint64_t bmask[kK2Blocks];           // AC non-zero mask (bit p = zig-zag position p); bit 0: ZRL block
+    uint32_t nzbase[kK2Blocks];          // first non-zero of each block in nz
+    uint32_t recbase[kK2Blocks];         // first record of each block in the tile's records
+    uint32_t rel[kK2Blocks];             // text index of each block (relative to the key bases)
+    int dcv[kK2Blocks];                  // DC of each block
+    uint8_t chroma[kK2Blocks];           // 1: a Cb / Cr block
+    uint8_t slotk[kK2Blocks];            // slot of each block in its MCU
+    uint32_t mcu[kK2Blocks];             // MCU of each block
     int prevdc[6];
-    uint32_t pcnt[kK2Threads];           // records of every part (stream order), then their offsets
     uint32_t wsum[kK2Threads / 64];
-    uint32_t recs[kTileRecords];         // the tile's symbol records, stream order
+    uint32_t tot;                        // the tile's non-zeros
+    // the workgroup's tiles: first block, and its MCU / slot / MCU row / column
+    uint32_t tb0[kK2MaxRun + 1], tm6[kK2MaxRun], tk[kK2MaxRun], trow[kK2MaxRun], tcol[kK2MaxRun];
 };
 
 // Record words (kernels.hpp): table << 24 | symbol << 16 | extra bits.
 __device__ __forceinline__ uint32_t rec_word(uint32_t table, uint32_t sym, uint32_t bits) {
     return (table << 24) | (sym << 16) | bits;
 }
+__device__ __forceinline__ uint32_t extra_bits(int v, int cat) {  // getCategoryAndCode, Coding.hpp:214-221
+    return (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1);
+}
 
+// K2 per tile, in four steps (barriers between them):
+//  A  each lane holds one natural-order row of a block: its zig-zag positions, the
+//     block's AC mask (OR over its 8 lanes), the DC;
+//  B  one lane per block: non-zeros, EOB, ZRL test (a zero run of 16 before the last
+//     non-zero: such blocks take the serial path), records; one scan gives every
+//     block's first non-zero and first record;
+//  C  each row lane files its AC non-zeros into nz at their stream rank;
+//  D  one lane per non-zero (all lanes busy whatever the block's density): run
+//     (from the block mask), category, symbol, histogram, first-occurrence key, its
+//     record at recbase + 1 + rank; one lane per block: DC, EOB, and the serial
+//     blocks' AC symbols with their ZRLs.
 __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     __shared__ K2Lds lds;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t mw = a.g.mw;
     // the entropy partition's tiles (seg_layout), a contiguous run per workgroup
     const uint32_t ntiles = seg_tiles(a.seg);
@@ -67,112 +103,235 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
     const uint32_t bpm = a.g.bpm, yh = a.g.yh, yv = a.g.yv();  // MCU = yh x yv Y blocks + Cb + Cr
     const uint64_t ybw = (uint64_t)mw * yh;                    // Y blocks per block row
     const uint32_t yhs = (uint32_t)__builtin_ctz(yh);          // yh is 1, 2 or 4: k / yh = k >> yhs
-    uint64_t fb0 = 0;
-    uint32_t fnb = 0;
-    if (t_first < t_last) seg_tile(a.seg, t_first, fb0, fnb);
-    const uint32_t mrow0 = (uint32_t)(fb0 / bpm) / mw;
+    // the tile table, computed once (64-bit arithmetic, one lane per tile)
+    const uint32_t nrun = t_last - t_first;
+    for (uint32_t i = tid; i <= nrun; i += kK2Threads) {
+        uint64_t tb;
+        uint32_t tn;
+        seg_tile(a.seg, min(t_first + i, ntiles - 1), tb, tn);
+        if (t_first + i >= ntiles) tb += tn;  // (the end of the last tile)
+        lds.tb0[i] = (uint32_t)tb;
+        if (i < nrun) {
+            const uint32_t m6 = (uint32_t)(tb / bpm);
+            lds.tm6[i] = m6;
+            lds.tk[i] = (uint32_t)(tb - (uint64_t)m6 * bpm);
+            lds.trow[i] = m6 / mw;
+            lds.tcol[i] = m6 % mw;
+        }
+    }
+    __syncthreads();
+    const uint64_t fb0 = nrun ? lds.tb0[0] : 0;
+    const uint32_t fnb = nrun ? lds.tb0[1] - lds.tb0[0] : 0;
+    const uint32_t mrow0 = nrun ? lds.trow[0] : 0;
     const uint64_t ybase = (uint64_t)mrow0 * yv * ybw;
     const uint64_t cbase = (uint64_t)mrow0 * mw;
-    const int lane = tid & 63, wv = tid >> 6;
-    const int blk = block_of(wv, lane), part = part_of(wv);
+    const float inv_bpm = 1.0f / (float)bpm, inv_mw = 1.0f / (float)mw;
+    const float inv_rst = a.rst.mcus ? 1.0f / (float)a.rst.mcus : 0.0f;
     TileRegs<kK2Threads, kK2Blocks> regs;
     regs.init(tid);
     if (t_first < t_last) regs.load(a.coef, fb0, (int)fnb, tid);
+    constexpr int kPer = TileRegs<kK2Threads, kK2Blocks>::kPer;
 
     uint64_t tq = JPGE_NOW();
     for (uint32_t tile = t_first; tile < t_last; ++tile) {
-        uint64_t b0;
-        uint32_t nbu;
-        seg_tile(a.seg, tile, b0, nbu);
-        const int nb = (int)nbu;
-        lds_barrier();  // previous tile's readers are done with zz / bmask / recs
-        regs.stage(nb, lds.zz, lds.bmask, lds.prevdc, tid);
-        if (tile + 1 < t_last) {  // (stays in flight across the LDS-only barriers below)
-            uint64_t nb0;
-            uint32_t nnb;
-            seg_tile(a.seg, tile + 1, nb0, nnb);
-            regs.load(a.coef, nb0, (int)nnb, tid);
-        }
-        lds_barrier();
-        JPGE_STAMP(1);
-        JPGE_ACC(0, tq);
-        const bool active = blk < nb;
-        const uint64_t g = b0 + blk;
-        const int k = (int)(g % bpm);
-        const uint64_t m6 = g / bpm;
-        const int comp = block_comp(k, bpm);
-        uint32_t rel;  // index of this block in its symbol text, relative to the bases
-        int tsel;
-        if (comp == 0) {
-            // raster index of Y slot k of MCU m6 (the Y text is in block raster order)
-            const uint32_t mrow = (uint32_t)(m6 / mw), mcol = (uint32_t)(m6 % mw);
-            rel = (uint32_t)(((uint64_t)mrow * yv + ((uint32_t)k >> yhs)) * ybw + (uint64_t)mcol * yh +
-                             ((uint32_t)k & (yh - 1)) - ybase);
-            tsel = 0;
-        } else {
-            rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);  // all Cr after all Cb
-            tsel = 1;
-        }
-        const uint64_t mask = lds.bmask[blk];
-        PartView pv;
-        pv.load(lds.zz, mask, blk, part, active);
-        const bool eob = active && part == 3 && !(mask >> 63);
-        // this part's records: DC, its ZRLs (only the first run of a 16-position part
-        // can reach 16) and run/size symbols, EOB — then its offset in the tile's stream
-        {
-            uint32_t n = 0;
-            if (active) {
-                n = (part == 0 ? 1u : 0u) + (uint32_t)__builtin_popcount(pv.m16) + (eob ? 1u : 0u);
-                if (pv.m16) n += (uint32_t)(16 * part + __builtin_ctz(pv.m16) - pv.last - 1) >> 4;
+        const uint32_t ti = tile - t_first;
+        const uint64_t b0 = lds.tb0[ti];
+        const int nb = (int)(lds.tb0[ti + 1] - lds.tb0[ti]);
+        uint32_t* grec = a.recs + (uint64_t)tile * kTileRecords;
+        lds_barrier();  // the previous tile's readers are done
+        // ---- A: masks and DCs ----
+        uint64_t rowbits[kPer];  // zig-zag positions of this lane's non-zero AC values
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int q = tid + i * kK2Threads;
+            const bool ok = q < nb * 8;
+            const int blk = q >> 3, row = q & 7;
+            const uint32_t w[4] = {regs.v[i].x, regs.v[i].y, regs.v[i].z, regs.v[i].w};
+            uint64_t m = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
+                const uint32_t zp = ((u < 4 ? regs.zlo : regs.zhi) >> (8 * (u & 3))) & 0xFF;
+                m |= (uint64_t)(ok && c != 0) << zp;
             }
-            lds.pcnt[blk * 4 + part] = n;
+            rowbits[i] = m & ~1ull;
+            m |= __shfl_xor(m, 1);
+            m |= __shfl_xor(m, 2);
+            m |= __shfl_xor(m, 4);
+            if (ok && row == 0) {
+                lds.bmask[blk] = m & ~1ull;
+                lds.dcv[blk] = (int16_t)(w[0] & 0xFFFF);
+            }
         }
+        if (tid < 6) lds.prevdc[tid] = regs.prev_dc;
         lds_barrier();
-        uint32_t T;  // the tile's records
-        const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(lds.pcnt[tid], lds.wsum, lane, wv, T);
-        lds.pcnt[tid] = ex;
+        JPGE_ACC(0, tq);
+        // ---- B: per block counts, ZRL test, key index; one scan ----
+        uint32_t cnt = 0;
+        const int b = tid;
+        const bool bact = b < nb;
+        int comp = 0;
+        if (bact) {
+            uint64_t m = lds.bmask[b];
+            const uint32_t n = (uint32_t)__builtin_popcountll(m);
+            const bool eob = !(m >> 63);
+            const uint64_t x = m | 1ull;
+            const int last = 63 - __builtin_clzll(x);
+            // a run of 16 zeros wholly before the last non-zero: a ZRL block
+            uint64_t z = ~x & ((last ? (1ull << last) : 1ull) - 1ull);
+            uint64_t r = z & (z >> 1);
+            r &= r >> 2;
+            r &= r >> 4;
+            r &= r >> 8;
+            uint32_t zrl = 0;
+            if (r) {  // rare: count the ZRLs serially
+                int prev = 0;
+                for (uint64_t t = m; t; t &= t - 1) {
+                    const int p = __builtin_ctzll(t);
+                    zrl += (uint32_t)(p - prev - 1) >> 4;
+                    prev = p;
+                }
+                lds.bmask[b] = m | 1ull;  // flag: the serial path codes its AC symbols
+            }
+            cnt = (n << 16) | (1u + n + zrl + (eob ? 1u : 0u));
+            // the block's MCU and slot, from the tile's (32-bit, small divisions)
+            uint32_t kk;
+            const uint32_t carry = udiv24(lds.tk[ti] + (uint32_t)b, bpm, inv_bpm, kk);
+            const int k = (int)kk;
+            const uint32_t m6 = lds.tm6[ti] + carry;
+            uint32_t mcol;
+            const uint32_t mrow = lds.trow[ti] + udiv24(lds.tcol[ti] + carry, mw, inv_mw, mcol);
+            comp = block_comp(k, bpm);
+            // the block's text index (the Y text is in block raster order; all Cr after all Cb)
+            uint32_t rel;
+            if (comp == 0) {
+                rel = (uint32_t)(((uint64_t)mrow * yv + ((uint32_t)k >> yhs)) * ybw + (uint64_t)mcol * yh +
+                                 ((uint32_t)k & (yh - 1)) - ybase);
+            } else {
+                rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
+            }
+            lds.rel[b] = rel;
+            lds.chroma[b] = comp != 0;
+            lds.slotk[b] = (uint8_t)k;
+            lds.mcu[b] = m6;
+        }
+        uint32_t T;
+        const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(cnt, lds.wsum, lane, wv, T);
+        if (bact) {
+            lds.nzbase[b] = ex >> 16;
+            lds.recbase[b] = ex & 0xFFFF;
+        }
+        if (tid == 0) {
+            lds.tot = T >> 16;
+            a.tcount[tile] = T & 0xFFFF;
+        }
         lds_barrier();
         JPGE_ACC(1, tq);
-        uint32_t o = lds.pcnt[blk * 4 + part];
-        if (active && part == 0) {  // DC symbol (difference to the chain predecessor)
-            const int dd = lds.zz[blk * kZzStride] - pred_dc(b0, blk, lds.zz, lds.prevdc, a.seed, a.rst, bpm);
+        // ---- C: the non-zeros at their stream rank ----
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int q = tid + i * kK2Threads;
+            const int blk = q >> 3;
+            uint64_t t = rowbits[i];
+            if (t) {
+                const uint64_t bm = lds.bmask[blk] & ~1ull;
+                const uint32_t base = lds.nzbase[blk];
+                const uint32_t w[4] = {regs.v[i].x, regs.v[i].y, regs.v[i].z, regs.v[i].w};
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
+                    const uint32_t zp = ((u < 4 ? regs.zlo : regs.zhi) >> (8 * (u & 3))) & 0xFF;
+                    if (zp != 0 && c != 0) {
+                        const uint32_t rank = (uint32_t)__builtin_popcountll(bm & ((1ull << zp) - 1ull));
+                        lds.nz[base + rank] = ((uint32_t)c & 0xFFFFu) | (zp << 16) | ((uint32_t)blk << 22);
+                    }
+                }
+            }
+        }
+        if (tile + 1 < t_last)  // the rows are filed: load the next tile's
+            regs.load(a.coef, lds.tb0[ti + 1], (int)(lds.tb0[ti + 2] - lds.tb0[ti + 1]), tid);
+        lds_barrier();
+        JPGE_ACC(2, tq);
+        // ---- D: symbols ----
+        const uint32_t N = lds.tot;
+        for (uint32_t e = tid; e < N; e += kK2Threads) {
+            const uint32_t ent = lds.nz[e];
+            const int v = (int16_t)(ent & 0xFFFF);
+            const int p = (int)((ent >> 16) & 63), blk = (int)(ent >> 22);
+            const uint64_t m = lds.bmask[blk];
+            if (m & 1ull) continue;  // ZRL block: the serial path
+            const int prev = 63 - __builtin_clzll((m | 1ull) & ((1ull << p) - 1ull));
+            const int run = p - prev - 1;  // < 16 here
+            const int cat = category(v);
+            const int sym = (run << 4) | cat;
+            const uint32_t rel = lds.rel[blk];
+            const int tsel = lds.chroma[blk];
+            atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + sym], 1u);
+            const uint32_t kk = ((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7)) + 2u * p + 1u;
+            uint32_t* kp = &lds.key[2 * tsel + 1][sym];
+            if (kk < *kp) atomicMin(kp, kk);
+            grec[lds.recbase[blk] + 1 + (e - lds.nzbase[blk])] = rec_word(2 * tsel + 1, (uint32_t)sym, extra_bits(v, cat));
+        }
+        if (bact) {  // one lane per block: DC, EOB, a serial block's AC symbols
+            const uint64_t m = lds.bmask[b];
+            const uint32_t rel = lds.rel[b];
+            const int tsel = comp != 0;
+            const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
+            uint32_t o = lds.recbase[b];
+            // DC difference to the chain predecessor (Image.cpp:638-678)
+            int pd;
+            {
+                const int k = lds.slotk[b];
+                bool reset = false;
+                if (a.rst.mcus && (k == 0 || k >= (int)bpm - 2)) {
+                    uint32_t r;
+                    udiv24(lds.mcu[b] + a.rst.mcu0, a.rst.mcus, inv_rst, r);
+                    reset = r == 0;
+                }
+                // the predecessor (dc_pred_index): the previous Y slot, 3 blocks back for an
+                // MCU's first Y block, bpm back for chroma; none in the first MCU
+                const bool ynext = k >= 1 && k < (int)bpm - 2;
+                const int back = ynext ? 1 : (k == 0 ? 3 : (int)bpm);
+                const int64_t pg = (!ynext && b0 + b < bpm) ? -1 : (int64_t)(b0 + b) - back;
+                pd = reset ? 0 : pg < 0 ? a.seed.v[block_comp(k, bpm)]
+                               : pg >= (int64_t)b0 ? lds.dcv[pg - (int64_t)b0] : lds.prevdc[pg - ((int64_t)b0 - 6)];
+            }
+            const int dd = lds.dcv[b] - pd;
             const int dcat = category(dd);
             atomicAdd(&lds.dcnt[lane & (kHistCopies - 1)][tsel * 16 + dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
-            const uint32_t db = (uint32_t)(dd < 0 ? dd + (1 << dcat) - 1 : dd) & ((1u << dcat) - 1);
-            lds.recs[o++] = rec_word(2 * tsel, (uint32_t)dcat, db);
-        }
-        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
-        uint32_t* cnt = &lds.acnt[lane & (kHistCopies - 1)][tsel * 256];
-        uint32_t* key = lds.key[2 * tsel + 1];
-        const uint32_t tac = 2 * tsel + 1;
-        for_each_ac(pv, part, [&](int p, int run, int v) {
-            const int cat = category(v);
-            const int sym = ((run & 15) << 4) | cat;
-            atomicAdd(&cnt[sym], 1u);
-            const uint32_t kk = acb + 2u * p + 1u;
-            if (kk < key[sym]) atomicMin(&key[sym], kk);
-            if (run >= 16) {
-                atomicAdd(&cnt[0xF0], (uint32_t)(run >> 4));
-                if (kk - 1u < key[0xF0]) atomicMin(&key[0xF0], kk - 1u);
-                for (int r = run; r >= 16; r -= 16) lds.recs[o++] = rec_word(tac, 0xF0, 0);
+            grec[o++] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
+            uint32_t* cntp = &lds.acnt[lane & (kHistCopies - 1)][tsel * 256];
+            uint32_t* key = lds.key[2 * tsel + 1];
+            const uint32_t tac = 2 * tsel + 1;
+            if (m & 1ull) {  // serial block: AC symbols with their ZRLs
+                const uint32_t nzb = lds.nzbase[b];
+                int prev = 0, r = 0;
+                for (uint64_t t = m & ~1ull; t; t &= t - 1, ++r) {
+                    const int p = __builtin_ctzll(t);
+                    int run = p - prev - 1;
+                    prev = p;
+                    const int v = (int16_t)(lds.nz[nzb + r] & 0xFFFF);
+                    const int cat = category(v);
+                    const uint32_t kk = acb + 2u * p + 1u;
+                    if (run >= 16) {
+                        atomicAdd(&cntp[0xF0], (uint32_t)(run >> 4));
+                        if (kk - 1u < key[0xF0]) atomicMin(&key[0xF0], kk - 1u);
+                        for (; run >= 16; run -= 16) grec[o++] = rec_word(tac, 0xF0, 0);
+                    }
+                    const int sym = (run << 4) | cat;
+                    atomicAdd(&cntp[sym], 1u);
+                    if (kk < key[sym]) atomicMin(&key[sym], kk);
+                    grec[o++] = rec_word(tac, (uint32_t)sym, extra_bits(v, cat));
+                }
             }
-            lds.recs[o++] = rec_word(tac, (uint32_t)sym, (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1));
-        });
-        if (eob) {
-            atomicAdd(&cnt[0], 1u);
-            if (acb + 127u < key[0]) atomicMin(&key[0], acb + 127u);
-            lds.recs[o] = rec_word(tac, 0, 0);
-        }
-        lds_barrier();
-        JPGE_ACC(2, tq);
-        // the tile's records to HBM, coalesced (16 bytes per lane)
-        {
-            uint4* dst = reinterpret_cast<uint4*>(a.recs + (uint64_t)tile * kTileRecords);
-            const uint4* src = reinterpret_cast<const uint4*>(lds.recs);
-            for (uint32_t i = tid; 4 * i < T; i += kK2Threads) dst[i] = src[i];
-            if (tid == 0) a.tcount[tile] = T;
+            if (!(m >> 63)) {  // EOB
+                atomicAdd(&cntp[0], 1u);
+                if (acb + 127u < key[0]) atomicMin(&key[0], acb + 127u);
+                const uint32_t eo = (b + 1 < nb ? lds.recbase[b + 1] : (T & 0xFFFF)) - 1;
+                grec[eo] = rec_word(tac, 0, 0);
+            }
         }
         JPGE_ACC(3, tq);
     }
@@ -229,7 +388,10 @@ hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* h
 
 uint32_t stats_grid(const SegLayout& L) {
     const uint32_t tiles = seg_tiles(L);
-    return tiles < 512 ? tiles : 512;  // 2 per CU, persistent over contiguous tiles
+    // 2 per CU, persistent over contiguous runs of at most kK2MaxRun tiles
+    const uint32_t g = tiles < 512 ? tiles : 512;
+    const uint32_t need = (tiles + kK2MaxRun - 1) / kK2MaxRun;
+    return g > need ? g : need;
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {

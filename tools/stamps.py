@@ -15,7 +15,7 @@ PHASES = {
     "entropy_pack": ["start", "scan", "output", "", "", "", "", ""],
 }
 ACC = {
-    "stats": ["stage", "count+scan", "symbols", "store"],
+    "stats": ["A masks", "B counts+scan", "C file", "D symbols"],
     "entropy_code": ["sync", "rounds(tail)", "store", "load+bits", "scan", "zero", "pack"],
 }
 
