@@ -352,6 +352,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->device_ = device;
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
     if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
+    if (const char* sw = std::getenv("JPGE_STATS_WGS")) e->stats_wgs_ = (uint32_t)std::strtoul(sw, nullptr, 10);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
@@ -510,6 +511,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs_);
     st.recs = s.d_recs;
     st.tcount = s.d_tcount;
+    st.wgs = stats_wgs_;
     st.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
     return st;
 }

@@ -147,6 +147,7 @@ class Encoder {
     std::atomic<uint64_t> seq_counter_{0};
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
+    uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
     int mode_ = 420;            // subsampling mode (jpge_set_subsampling)
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs_); }

@@ -158,6 +158,7 @@ struct StatsArgs {
     SegLayout seg;       // the entropy partition: the tiles the records are written in
     uint32_t* recs;      // [tiles][kTileRecords] symbol records
     uint32_t* tcount;    // [tiles] records per tile
+    uint32_t wgs = 0;    // workgroup count override (0 = automatic; diagnostics)
     uint64_t* dbg;
 };
 

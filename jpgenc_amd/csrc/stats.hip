@@ -53,6 +53,7 @@ struct K2Lds {
     uint32_t dcnt[kHistCopies][kDcCopyWords];  // DC counters (Y-DC at 0, C-DC at 16), per copy
     uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
     uint64_t bmask[kK2Blocks];           // AC non-zero mask (bit p = zig-zag position p); bit 0: ZRL block
+    uint64_t lmask[kK2Blocks];           // ZRL block: the non-zeros after a run of 16+ zeros
     uint32_t nzbase[kK2Blocks];          // first non-zero of each block in nz
     uint32_t recbase[kK2Blocks];         // first record of each block in the tile's records
     uint32_t rel[kK2Blocks];             // text index of each block (relative to the key bases)
@@ -184,14 +185,14 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
             r &= r >> 4;
             r &= r >> 8;
             uint32_t zrl = 0;
-            if (r) {  // rare: count the ZRLs serially
-                int prev = 0;
-                for (uint64_t t = m; t; t &= t - 1) {
+            if (r) {  // rare: the non-zeros after a run of 16+ zeros, and their ZRL count
+                const uint64_t L = m & (r << 16);
+                for (uint64_t t = L; t; t &= t - 1) {
                     const int p = __builtin_ctzll(t);
-                    zrl += (uint32_t)(p - prev - 1) >> 4;
-                    prev = p;
+                    zrl += (uint32_t)(p - (63 - __builtin_clzll(x & ((1ull << p) - 1ull))) - 1) >> 4;
                 }
-                lds.bmask[b] = m | 1ull;  // flag: the serial path codes its AC symbols
+                lds.bmask[b] = m | 1ull;  // flag: a ZRL block
+                lds.lmask[b] = L;
             }
             cnt = (n << 16) | (1u + n + zrl + (eob ? 1u : 0u));
             // the block's MCU and slot, from the tile's (32-bit, small divisions)
@@ -259,9 +260,16 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
             const int v = (int16_t)(ent & 0xFFFF);
             const int p = (int)((ent >> 16) & 63), blk = (int)(ent >> 22);
             const uint64_t m = lds.bmask[blk];
-            if (m & 1ull) continue;  // ZRL block: the serial path
-            const int prev = 63 - __builtin_clzll((m | 1ull) & ((1ull << p) - 1ull));
-            const int run = p - prev - 1;  // < 16 here
+            int run = p - (63 - __builtin_clzll((m | 1ull) & ((1ull << p) - 1ull))) - 1;
+            uint32_t zb = 0;  // ZRL records of this block up to and including this entry's
+            if (m & 1ull) {   // a ZRL block (rare): the long runs at or before p
+                for (uint64_t t = lds.lmask[blk] & (((1ull << p) - 1ull) | (1ull << p)); t; t &= t - 1) {
+                    const int q = __builtin_ctzll(t);
+                    zb += (uint32_t)(q - (63 - __builtin_clzll(m & ((1ull << q) - 1ull))) - 1) >> 4;
+                }
+            }
+            const int nzr = run >> 4;
+            run &= 15;
             const int cat = category(v);
             const int sym = (run << 4) | cat;
             const uint32_t rel = lds.rel[blk];
@@ -270,14 +278,20 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
             const uint32_t kk = ((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7)) + 2u * p + 1u;
             uint32_t* kp = &lds.key[2 * tsel + 1][sym];
             if (kk < *kp) atomicMin(kp, kk);
-            grec[lds.recbase[blk] + 1 + (e - lds.nzbase[blk])] = rec_word(2 * tsel + 1, (uint32_t)sym, extra_bits(v, cat));
+            const uint32_t o = lds.recbase[blk] + 1 + (e - lds.nzbase[blk]) + zb;
+            if (nzr) {  // its ZRLs (F/0) just before it
+                atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + 0xF0], (uint32_t)nzr);
+                uint32_t* kz = &lds.key[2 * tsel + 1][0xF0];
+                if (kk - 1u < *kz) atomicMin(kz, kk - 1u);
+                for (int z = 1; z <= nzr; ++z) grec[o - z] = rec_word(2 * tsel + 1, 0xF0, 0);
+            }
+            grec[o] = rec_word(2 * tsel + 1, (uint32_t)sym, extra_bits(v, cat));
         }
-        if (bact) {  // one lane per block: DC, EOB, a serial block's AC symbols
+        if (bact) {  // one lane per block: DC and EOB
             const uint64_t m = lds.bmask[b];
             const uint32_t rel = lds.rel[b];
             const int tsel = comp != 0;
             const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
-            uint32_t o = lds.recbase[b];
             // DC difference to the chain predecessor (Image.cpp:638-678)
             int pd;
             {
@@ -301,36 +315,13 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
             atomicAdd(&lds.dcnt[lane & (kHistCopies - 1)][tsel * 16 + dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
-            grec[o++] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
-            uint32_t* cntp = &lds.acnt[lane & (kHistCopies - 1)][tsel * 256];
-            uint32_t* key = lds.key[2 * tsel + 1];
-            const uint32_t tac = 2 * tsel + 1;
-            if (m & 1ull) {  // serial block: AC symbols with their ZRLs
-                const uint32_t nzb = lds.nzbase[b];
-                int prev = 0, r = 0;
-                for (uint64_t t = m & ~1ull; t; t &= t - 1, ++r) {
-                    const int p = __builtin_ctzll(t);
-                    int run = p - prev - 1;
-                    prev = p;
-                    const int v = (int16_t)(lds.nz[nzb + r] & 0xFFFF);
-                    const int cat = category(v);
-                    const uint32_t kk = acb + 2u * p + 1u;
-                    if (run >= 16) {
-                        atomicAdd(&cntp[0xF0], (uint32_t)(run >> 4));
-                        if (kk - 1u < key[0xF0]) atomicMin(&key[0xF0], kk - 1u);
-                        for (; run >= 16; run -= 16) grec[o++] = rec_word(tac, 0xF0, 0);
-                    }
-                    const int sym = (run << 4) | cat;
-                    atomicAdd(&cntp[sym], 1u);
-                    if (kk < key[sym]) atomicMin(&key[sym], kk);
-                    grec[o++] = rec_word(tac, (uint32_t)sym, extra_bits(v, cat));
-                }
-            }
+            grec[lds.recbase[b]] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
             if (!(m >> 63)) {  // EOB
-                atomicAdd(&cntp[0], 1u);
-                if (acb + 127u < key[0]) atomicMin(&key[0], acb + 127u);
+                atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256], 1u);
+                uint32_t* ke = &lds.key[2 * tsel + 1][0];
+                if (acb + 127u < *ke) atomicMin(ke, acb + 127u);
                 const uint32_t eo = (b + 1 < nb ? lds.recbase[b + 1] : (T & 0xFFFF)) - 1;
-                grec[eo] = rec_word(tac, 0, 0);
+                grec[eo] = rec_word(2 * tsel + 1, 0, 0);
             }
         }
         JPGE_ACC(3, tq);
@@ -395,7 +386,12 @@ uint32_t stats_grid(const SegLayout& L) {
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(stats_kernel, dim3(stats_grid(a.seg)), dim3(kK2Threads), 0, s, a);
+    uint32_t g = stats_grid(a.seg);
+    if (a.wgs) {  // (diagnostic override, kept within the tile-table bound)
+        const uint32_t need = (seg_tiles(a.seg) + kK2MaxRun - 1) / kK2MaxRun;
+        g = a.wgs < need ? need : (a.wgs > seg_tiles(a.seg) ? seg_tiles(a.seg) : a.wgs);
+    }
+    hipLaunchKernelGGL(stats_kernel, dim3(g), dim3(kK2Threads), 0, s, a);
     return hipGetLastError();
 }
 
