@@ -71,7 +71,6 @@ __device__ __forceinline__ int category(int v) {
     return av ? 32 - __builtin_clz((unsigned)av) : 0;
 }
 
-constexpr int kZzStride = 72;      // int16 per staged block in LDS (144 B: spreads banks)
 constexpr int kPartsPerBlock = 4;  // lanes cooperating on one block's non-zero coefficients
 
 // DC predecessor of flat block g (Image.cpp:638-678): the Y chain runs in MCU
@@ -117,51 +116,7 @@ struct TileRegs {
         }
         prev_dc = (tid < 6 && b0 + tid >= 6) ? coef[(b0 - 6 + tid) * 64] : 0;
     }
-
-    // zig-zag-ordered LDS blocks, the AC non-zero mask of every block (bit p =
-    // zig-zag position p, OR-reduced over the 8 lanes of the block) and the DCs of
-    // the 6 blocks before the tile (prevdc[i] = DC of block b0 - 6 + i)
-    __device__ __forceinline__ void stage(int nb, int16_t* zz, uint64_t* bmask, int* prevdc, int tid) const {
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            const int q = tid + i * kThreads;
-            const bool ok = q < nb * 8;
-            const int blk = q >> 3, row = q & 7;
-            uint64_t m = 0;
-            if (ok) {
-                int16_t* d = zz + blk * kZzStride;
-                const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
-                    const uint32_t zp = ((u < 4 ? zlo : zhi) >> (8 * (u & 3))) & 0xFF;
-                    d[zp] = c;
-                    m |= (uint64_t)(c != 0) << zp;
-                }
-            }
-            m |= __shfl_xor(m, 1);
-            m |= __shfl_xor(m, 2);
-            m |= __shfl_xor(m, 4);
-            if (ok && row == 0) bmask[blk] = m & ~1ull;  // AC only
-        }
-        if (tid < 6) prevdc[tid] = prev_dc;
-    }
 };
-
-// DC of the chain predecessor of block b0+blk (0 for a chain's first block and at a
-// restart interval's start), from the staged tile or the 6 DCs staged before it.
-__device__ __forceinline__ int pred_dc(uint64_t b0, int blk, const int16_t* zz, const int* prevdc,
-                                       const DcSeed& seed, const Restart& rs, uint32_t bpm) {
-    const uint64_t g = b0 + blk;
-    const int k = (int)(g % bpm);
-    if (rs.mcus) {  // a restart interval's first MCU: its first Y, Cb and Cr predict 0 again
-        if ((k == 0 || k >= (int)bpm - 2) && (g / bpm + rs.mcu0) % rs.mcus == 0) return 0;
-    }
-    const int64_t pg = dc_pred_index(g, bpm);
-    if (pg < 0) return seed.v[block_comp(k, bpm)];  // first MCU: 0, or the previous stripe's last DC
-    if (pg >= (int64_t)b0) return zz[(pg - (int64_t)b0) * kZzStride];
-    return prevdc[pg - ((int64_t)b0 - 6)];
-}
 
 // Workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not
 // for its global loads or stores.  __syncthreads() is a workgroup fence as well,
@@ -175,46 +130,6 @@ __device__ __forceinline__ void lds_barrier() {
 // Wait for this lane's outstanding global stores (so a following barrier publishes
 // them to the rest of the workgroup).
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Lane mapping of the symbol kernels (K2, K3): a 512-thread workgroup codes a
-// tile of 128 blocks; wave w covers zig-zag positions [16q, 16q+16), q = w & 3
-// (the "part"), of the 64 blocks (w >> 2) * 64 + lane.  All lanes of a wave visit
-// the same positions, so a position no lane has a non-zero at is skipped by the
-// whole wave.  Stream order of the parts is block-major: index blk * 4 + part.
-__device__ __forceinline__ int part_of(int wv) { return wv & 3; }
-__device__ __forceinline__ int block_of(int wv, int lane) { return (wv >> 2) * 64 + lane; }
-
-struct PartView {
-    uint32_t m16;        // AC non-zero bits of the part's 16 positions (bit i = position 16*part + i)
-    int last;            // zig-zag position of the last non-zero before the part (0 = DC)
-    const int16_t* row;  // the part's 16 staged coefficients (LDS)
-
-    __device__ __forceinline__ void load(const int16_t* zz, uint64_t mask, int blk, int part, bool active) {
-        row = zz + blk * kZzStride + 16 * part;
-        if (!active) mask = 0;
-        m16 = (uint32_t)(mask >> (16 * part)) & 0xFFFFu;
-        const uint64_t below = part ? mask & ((1ull << (16 * part)) - 1) : 0ull;
-        last = below ? 63 - __builtin_clzll(below) : 0;
-    }
-};
-
-// f(p, run, v) for every non-zero AC coefficient of the part, in zig-zag order
-// (run = zeros since the previous non-zero of the block, may be >= 16).  A wave
-// iterates max-over-lanes popcount(m16) times.
-template <typename F>
-__device__ __forceinline__ void for_each_ac(const PartView& pv, int part, F&& f) {
-    uint32_t m = pv.m16;
-    int last = pv.last;
-    while (__ballot(m != 0)) {
-        if (m) {
-            const int i = __builtin_ctz(m);
-            m &= m - 1;
-            const int p = 16 * part + i;
-            f(p, p - last - 1, (int)pv.row[i]);
-            last = p;
-        }
-    }
-}
 
 // Histogram export: sum the replicas and write the four final histograms and
 // first-occurrence keys into mapped host memory, then the frame's sequence number

@@ -89,7 +89,6 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4)))
     EntropyArgs a) {
     __shared__ K3Lds L;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int blk = block_of(wv, lane), part = part_of(wv);
     const uint32_t wg = blockIdx.x;
     JPGE_STAMP(0);
     if (a.exp_cnt && wg == 0)  // carried: a later frame's histograms to the host

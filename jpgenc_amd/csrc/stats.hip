@@ -5,8 +5,8 @@
 // code kernel turns into bits once the tables exist: the run-length and category
 // work is done once per frame.
 //
-// Lane mapping: PartView (device_common.hpp), four lanes per block, one wave per
-// 16 zig-zag positions of 64 blocks.  Persistent grid:
+// Lane mapping (per step, below): a block row per lane, a block per lane, a
+// non-zero per lane.  Persistent grid:
 // each workgroup owns a contiguous run of 128-block tiles (the next one is loaded
 // into registers while the current one is counted), accumulates into LDS
 // (8 bank-staggered copies of the AC counters cap same-address atomics at 8 lanes) and flushes
