@@ -678,10 +678,12 @@ def run_frames(args, rank, local, world, pg):
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H) if args.subsampling == 420 else {}
     yh, yv = J.SUBSAMPLING[args.subsampling]
     cb = 2.0 * 64 * (yh * yv + 2) / (64 * yh * yv)  # int16 coefficient bytes per pixel (4:2:0: 3)
+    # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3
+    rec_bytes = 4.0 * tm["symbols"] / max(1, tm["frames"])
     alg = {
         "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
-        "stats_kernel": (cb * npx, f"coefficients read {cb:g} B/px"),
-        "entropy_kernel": (cb * npx + avg_jpeg, f"coefficients read {cb:g} B/px + entropy-coded bytes written"),
+        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 4 B each"),
+        "entropy_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + entropy-coded bytes written"),
     }
 
     def rooflines(tm):

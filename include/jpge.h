@@ -63,6 +63,7 @@ typedef struct {
     float total;    /* K1 start .. K3 end of that frame (includes the queued work of other frames) */
     double fdct_sum, dc_stats_sum, entropy_sum; /* accumulated since jpge_reset_timing (ms) */
     uint64_t frames;                            /* frames accumulated */
+    uint64_t symbols; /* Huffman-coded symbols of those frames (= K2's 4-byte symbol records) */
 } jpge_timing;
 
 const char* jpge_strerror(int status);

@@ -93,6 +93,7 @@ int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
     t->dc_stats_sum = k.dc_stats_sum;
     t->entropy_sum = k.entropy_sum;
     t->frames = k.frames;
+    t->symbols = k.symbols;
     return JPGE_OK;
 }
 

@@ -234,6 +234,7 @@ struct Encoder::Slot {
     uint8_t* out_dev = nullptr;
     size_t out_cap = 0;
     size_t hdr_len = 0;
+    uint64_t symbols = 0;              // Huffman-coded symbols (= K2 symbol records) of the frame
     uint8_t qy[64], qc[64];
     bool timed = false;                // this frame's kernels are bracketed by timing events
     HistPtrs hist{};                   // this frame's device histograms (in d_ctl)
@@ -643,6 +644,9 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
         ok[t] = 1;
     });
     const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
+    uint64_t nsym = 0;
+    for (int i = 0; i < 1024; ++i) nsym += cnt_all[i];
+    s.symbols = nsym;
     if (bad) return kErrInternal;
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
     const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_,
@@ -689,6 +693,7 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
         times_.dc_stats_sum += times_.dc_stats;
         times_.entropy_sum += times_.entropy;
         times_.frames += 1;
+        times_.symbols += s.symbols;
     }
     if (stamps_file_) hipStreamSynchronize(s.stream);
     dump_stamps(s);

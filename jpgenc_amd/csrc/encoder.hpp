@@ -38,6 +38,7 @@ struct KernelTimes {  // milliseconds of the last timed frame (HIP events on the
     float fdct = 0, dc_stats = 0, entropy = 0, total = 0;
     double fdct_sum = 0, dc_stats_sum = 0, entropy_sum = 0;  // accumulated since reset
     uint64_t frames = 0;
+    uint64_t symbols = 0;  // Huffman-coded symbols of the timed frames
 };
 
 class Encoder {

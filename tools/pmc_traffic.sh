@@ -15,4 +15,4 @@ for set in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set --output-format csv -d "$out" -o pass$i -- \
     python3 "$R/bench.py" --no-cpu-baseline "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
 done
-python3 "$R/tools/pmc_summary.py" "$out" --json "$R/gpurun_out/pmc_$tag.json"
+python3 "$R/tools/pmc_summary.py" "$out" --json "$R/gpurun_out/pmc_$tag.json" --width "${PMC_W:-3840}" --height "${PMC_H:-2160}"
