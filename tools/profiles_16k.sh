@@ -16,3 +16,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 python3 tools/rocprof_window.py gpurun_out/p16/trace gpurun_out/p16/prof_bench.json | tee gpurun_out/p16/window.txt
 PMC_W=16384 PMC_H=16384 bash tools/pmc_traffic.sh 16k $A || exit 1
 python3 tools/pmc_summary.py gpurun_out/pmc_16k | tail -20
+find gpurun_out/p16/trace gpurun_out/pmc_16k -name '*kernel_trace.csv' -delete 2>/dev/null
+find gpurun_out/pmc_16k -name '*counter_collection.csv' -exec gzip -9 {} + 2>/dev/null
+true

@@ -16,3 +16,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 python3 tools/rocprof_window.py gpurun_out/rp/trace gpurun_out/rp/prof_bench.json | tee gpurun_out/rp/window.txt
 bash tools/pmc_traffic.sh rp || exit 1
 python3 tools/pmc_summary.py gpurun_out/pmc_rp | tail -40
+# keep the summaries (gpurun copies back <= 64 MiB): drop the per-dispatch CSVs
+find gpurun_out/rp/trace gpurun_out/pmc_rp -name '*kernel_trace.csv' -delete 2>/dev/null
+find gpurun_out/pmc_rp -name '*counter_collection.csv' -exec gzip -9 {} + 2>/dev/null
+true
