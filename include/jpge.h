@@ -165,8 +165,9 @@ int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t*
 
 /* huffmanDecode (Huffman.hpp:62, Huffman.cpp:91-146): the symbol text coded in the
  * first nbits bits (MSB-first bytes) by the table of nsym (symbol, code, length)
- * entries, codes right-aligned as jpge_huffman_text returns them.  text = NULL:
- * count only.  JPGE_E_FORMAT where no code matches (the reference asserts). */
+ * entries, codes right-aligned as jpge_huffman_text returns them.  `bits` must hold
+ * at least ceil(nbits / 8) bytes.  text = NULL: count only.  JPGE_E_FORMAT where no
+ * code matches (the reference asserts). */
 int jpge_huffman_decode(const uint8_t* bits, uint64_t nbits, const uint32_t* table_syms, const uint32_t* table_codes,
                         const uint8_t* table_lens, int nsym, int* text, size_t cap, size_t* n);
 

@@ -216,12 +216,14 @@ int jpge_decode_coeffs(const uint8_t* jpg, size_t len, jpge_decoded* info, int16
                 o += 17 + (uint32_t)nsym;
             }
         } else if (m == 0xDD) {  // DRI
+            if (sl < 4) return JPGE_E_FORMAT;
             restart = be16(s);
         } else if (m == 0xDA) {  // SOS: three components, in frame order
-            if (!sof || s[0] != 3) return JPGE_E_FORMAT;
+            if (!sof || sl < 2 + 1 + 2 * 3 + 3 || s[0] != 3) return JPGE_E_FORMAT;
             for (int c = 0; c < 3; ++c) {
                 td[c] = s[2 + 2 * c] >> 4;
                 ta[c] = s[2 + 2 * c] & 15;
+                if (td[c] > 3 || ta[c] > 3) return JPGE_E_FORMAT;
             }
             pos += 2 + sl;
             break;

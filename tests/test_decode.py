@@ -122,3 +122,37 @@ def test_decode_coeffs_rejects_garbage():
     data = bytearray(_oracle.encode(J.synth_rgb8(1, 40, 40), 90))
     with pytest.raises(J.JpgeError):  # truncated entropy data
         J.decode_coeffs(bytes(data[: len(data) // 2]))
+
+
+def _segment(data, marker):
+    """Offset of the first marker segment `marker` (0xFF <marker>) in a header."""
+    pos = 2
+    while pos + 4 <= len(data):
+        assert data[pos] == 0xFF
+        if data[pos + 1] == marker:
+            return pos
+        pos += 2 + (data[pos + 2] << 8 | data[pos + 3])
+    raise AssertionError("segment not found")
+
+
+def test_decode_coeffs_rejects_short_segments():
+    # DRI / SOS segments whose declared length is too short, and table selectors past
+    # the four table slots, are format errors (no read past the segment)
+    data = _oracle.encode(J.synth_rgb8(3, 48, 32), 90, restart=2)
+    assert J.decode_coeffs(data)[0].restart == 2
+    bad = bytearray(data)
+    p = _segment(bad, 0xDD)
+    bad[p + 2:p + 4] = b"\x00\x02"  # DRI length 2: no interval field
+    bad[p + 4:p + 6] = b"\xff\xfe"  # (the old field now reads as the next segment's marker: COM)
+    with pytest.raises(J.JpgeError):
+        J.decode_coeffs(bytes(bad))
+    bad = bytearray(data)
+    p = _segment(bad, 0xDA)
+    bad[p + 2:p + 4] = b"\x00\x08"  # SOS length 8 < 12
+    with pytest.raises(J.JpgeError):
+        J.decode_coeffs(bytes(bad))
+    bad = bytearray(data)
+    p = _segment(bad, 0xDA)
+    bad[p + 4 + 2] = 0x07  # Y: DC table 0, AC table 7
+    with pytest.raises(J.JpgeError):
+        J.decode_coeffs(bytes(bad))
