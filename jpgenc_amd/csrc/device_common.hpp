@@ -151,6 +151,19 @@ __device__ __forceinline__ void export_hist(const HistPtrs& h, uint32_t* host_cn
     }
 }
 
+// Inclusive scan of one u32 per lane over the wave in DPP moves (row shifts, then
+// the row broadcasts of lanes 15 and 31): no LDS traffic, no waits.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)x;
+}
+
 // block-wide exclusive scan of one value per thread (thread order); wsum holds
 // kWaves values of T.  kLdsSync: LDS-only barriers (lds_barrier), so global loads in
 // flight stay in flight.

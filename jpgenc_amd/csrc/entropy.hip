@@ -28,6 +28,9 @@ namespace jpge {
 namespace {
 using namespace dev;
 
+#ifndef K3_WPE
+#define K3_WPE 4
+#endif
 #ifndef K3_ZERO_TILE
 #define K3_ZERO_TILE 0
 #endif
@@ -85,7 +88,7 @@ __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, ui
     return (ent >> 16) + nb;
 }
 
-__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(4))) void entropy_code_kernel(
+__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_WPE))) void entropy_code_kernel(
     EntropyArgs a) {
     __shared__ K3Lds L;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
