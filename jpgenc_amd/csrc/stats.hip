@@ -9,7 +9,7 @@
 // non-zero per lane.  Persistent grid:
 // each workgroup owns a contiguous run of 128-block tiles (the next one is loaded
 // into registers while the current one is counted), accumulates into LDS
-// (8 bank-staggered copies of the AC counters cap same-address atomics at 8 lanes) and flushes
+// (bank-staggered copies of the counters split same-address atomics) and flushes
 // once into kHistReplicas global replicas.  First-occurrence keys (text index of
 // the symbol, see huffman.hpp) are kept workgroup-relative in u32 LDS words and
 // widened at the flush; the global key is stored inverted so atomicMax keeps the
@@ -22,19 +22,27 @@ using namespace dev;
 
 constexpr int kK2Blocks = kStatsTile;
 constexpr int kK2Threads = kK2Blocks * kPartsPerBlock;
-constexpr int kHistCopies = 8;
+#ifndef K2_COPIES
+#define K2_COPIES 4
+#endif
+constexpr int kHistCopies = K2_COPIES;
 // Copy stride 512 + 4 words: LDS atomics bank by (word mod 32), so an unpadded
 // stride (512) put every copy of a symbol on one bank and the copies only turned
-// same-address serialisation into same-bank conflicts.  With +4 the 8 copies of a
-// symbol sit on banks s, s+4, ..., s+28 (bank-conflict cycles halved; 16 copies at
-// +2 removed only 7% more and cost LDS occupancy in the pipeline).
+// same-address serialisation into same-bank conflicts.  With +4 the copies of a
+// symbol sit on banks s, s+4, ... (bank-conflict cycles halved).  4 copies, not 8:
+// the 8.3 KB saved (with the shorter tile table) brings the workgroup to 52.7 KB,
+// 3 per CU (6 waves per SIMD with <= 80 VGPRs): +5% in the pipeline, solo unchanged.
 constexpr int kCopyWords = 2 * 256 + 4;
 // DC counters: one wave's 64 lanes count a handful of categories; the same copies
 // and bank stagger (stride 36 words) split them.
 constexpr int kDcCopyWords = 2 * 16 + 4;
 
 constexpr int kMaxNz = kK2Blocks * 63;  // AC non-zeros of a tile, at most
-constexpr int kK2MaxRun = 256;           // tiles per workgroup, at most (stats_grid)
+#ifndef K2_PERCU
+#define K2_PERCU 3
+#endif
+constexpr int kK2PerCu = K2_PERCU;        // resident workgroups per CU (stats_grid)
+constexpr int kK2MaxRun = kK2PerCu > 2 ? 128 : 256;  // tiles per workgroup, at most (stats_grid)
 
 // x / d and x % d for x < 2^24 (float reciprocal, corrected): the index arithmetic
 // stays in 32-bit registers (a 64-bit division costs ~100 instructions per lane)
@@ -87,7 +95,7 @@ __device__ __forceinline__ uint32_t extra_bits(int v, int cat) {  // getCategory
 //     (from the block mask), category, symbol, histogram, first-occurrence key, its
 //     record at recbase + 1 + rank; one lane per block: DC, EOB, and the serial
 //     blocks' AC symbols with their ZRLs.
-__global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
+__global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(StatsArgs a) {
     __shared__ K2Lds lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t mw = a.g.mw;
@@ -141,6 +149,9 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         uint32_t* grec = a.recs + (uint64_t)tile * kTileRecords;
         lds_barrier();  // the previous tile's readers are done
         // ---- A: masks and DCs ----
+        // (zlo/zhi made opaque per tile: the compiler would otherwise keep 8 zig-zag
+        // positions and 8 64-bit masks derived from them live across the whole loop)
+        asm volatile("" : "+v"(regs.zlo), "+v"(regs.zhi));
         uint64_t rowbits[kPer];  // zig-zag positions of this lane's non-zero AC values
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
@@ -229,6 +240,7 @@ __global__ __launch_bounds__(kK2Threads) void stats_kernel(StatsArgs a) {
         lds_barrier();
         JPGE_ACC(1, tq);
         // ---- C: the non-zeros at their stream rank ----
+        asm volatile("" : "+v"(regs.zlo), "+v"(regs.zhi));
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const int q = tid + i * kK2Threads;
@@ -379,8 +391,8 @@ hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* h
 
 uint32_t stats_grid(const SegLayout& L) {
     const uint32_t tiles = seg_tiles(L);
-    // 2 per CU, persistent over contiguous runs of at most kK2MaxRun tiles
-    const uint32_t g = tiles < 512 ? tiles : 512;
+    // kK2PerCu per CU, persistent over contiguous runs of at most kK2MaxRun tiles
+    const uint32_t g = tiles < 256u * kK2PerCu ? tiles : 256u * kK2PerCu;
     const uint32_t need = (tiles + kK2MaxRun - 1) / kK2MaxRun;
     return g > need ? g : need;
 }
