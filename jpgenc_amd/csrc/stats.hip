@@ -20,8 +20,15 @@ namespace jpge {
 namespace {
 using namespace dev;
 
-constexpr int kK2Blocks = kStatsTile;
-constexpr int kK2Threads = kK2Blocks * kPartsPerBlock;
+#ifndef K2_STEP
+#define K2_STEP 128
+#endif
+// Blocks per step: a tile is counted in steps of kK2Blocks.  64-block steps (34 KB,
+// 63 VGPRs: 4 workgroups per CU) ran 3.5% slower in the pipeline than whole tiles at
+// 3 per CU: the per-step barrier skeleton outweighs the occupancy.
+constexpr int kK2Blocks = K2_STEP;
+constexpr int kK2Threads = 512;
+static_assert(kEntropyTile % kK2Blocks == 0, "steps divide a tile");
 #ifndef K2_COPIES
 #define K2_COPIES 4
 #endif
@@ -138,16 +145,20 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
     const float inv_rst = a.rst.mcus ? 1.0f / (float)a.rst.mcus : 0.0f;
     TileRegs<kK2Threads, kK2Blocks> regs;
     regs.init(tid);
-    if (t_first < t_last) regs.load(a.coef, fb0, (int)fnb, tid);
+    if (t_first < t_last) regs.load(a.coef, fb0, min((int)fnb, kK2Blocks), tid);
     constexpr int kPer = TileRegs<kK2Threads, kK2Blocks>::kPer;
 
     uint64_t tq = JPGE_NOW();
     for (uint32_t tile = t_first; tile < t_last; ++tile) {
         const uint32_t ti = tile - t_first;
-        const uint64_t b0 = lds.tb0[ti];
-        const int nb = (int)(lds.tb0[ti + 1] - lds.tb0[ti]);
+        const uint64_t tb = lds.tb0[ti];
+        const int tnb = (int)(lds.tb0[ti + 1] - lds.tb0[ti]);
         uint32_t* grec = a.recs + (uint64_t)tile * kTileRecords;
-        lds_barrier();  // the previous tile's readers are done
+        uint32_t rec0 = 0;  // the tile's records before this step
+      for (int s0 = 0; s0 < tnb; s0 += kK2Blocks) {
+        const uint64_t b0 = tb + (uint64_t)s0;
+        const int nb = min(tnb - s0, kK2Blocks);
+        lds_barrier();  // the previous step's readers are done
         // ---- A: masks and DCs ----
         // (zlo/zhi made opaque per tile: the compiler would otherwise keep 8 zig-zag
         // positions and 8 64-bit masks derived from them live across the whole loop)
@@ -208,7 +219,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             cnt = (n << 16) | (1u + n + zrl + (eob ? 1u : 0u));
             // the block's MCU and slot, from the tile's (32-bit, small divisions)
             uint32_t kk;
-            const uint32_t carry = udiv24(lds.tk[ti] + (uint32_t)b, bpm, inv_bpm, kk);
+            const uint32_t carry = udiv24(lds.tk[ti] + (uint32_t)(s0 + b), bpm, inv_bpm, kk);
             const int k = (int)kk;
             const uint32_t m6 = lds.tm6[ti] + carry;
             uint32_t mcol;
@@ -231,12 +242,9 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
         const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(cnt, lds.wsum, lane, wv, T);
         if (bact) {
             lds.nzbase[b] = ex >> 16;
-            lds.recbase[b] = ex & 0xFFFF;
+            lds.recbase[b] = rec0 + (ex & 0xFFFF);
         }
-        if (tid == 0) {
-            lds.tot = T >> 16;
-            a.tcount[tile] = T & 0xFFFF;
-        }
+        if (tid == 0) lds.tot = T >> 16;
         lds_barrier();
         JPGE_ACC(1, tq);
         // ---- C: the non-zeros at their stream rank ----
@@ -261,8 +269,10 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                 }
             }
         }
-        if (tile + 1 < t_last)  // the rows are filed: load the next tile's
-            regs.load(a.coef, lds.tb0[ti + 1], (int)(lds.tb0[ti + 2] - lds.tb0[ti + 1]), tid);
+        if (s0 + kK2Blocks < tnb)  // the rows are filed: load the next step's
+            regs.load(a.coef, b0 + kK2Blocks, min(tnb - s0 - kK2Blocks, kK2Blocks), tid);
+        else if (tile + 1 < t_last)
+            regs.load(a.coef, lds.tb0[ti + 1], min((int)(lds.tb0[ti + 2] - lds.tb0[ti + 1]), kK2Blocks), tid);
         lds_barrier();
         JPGE_ACC(2, tq);
         // ---- D: symbols ----
@@ -332,11 +342,14 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                 atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256], 1u);
                 uint32_t* ke = &lds.key[2 * tsel + 1][0];
                 if (acb + 127u < *ke) atomicMin(ke, acb + 127u);
-                const uint32_t eo = (b + 1 < nb ? lds.recbase[b + 1] : (T & 0xFFFF)) - 1;
+                const uint32_t eo = (b + 1 < nb ? lds.recbase[b + 1] : rec0 + (T & 0xFFFF)) - 1;
                 grec[eo] = rec_word(2 * tsel + 1, 0, 0);
             }
         }
         JPGE_ACC(3, tq);
+        rec0 += T & 0xFFFF;
+      }
+        if (tid == 0) a.tcount[tile] = rec0;
     }
     __syncthreads();
     JPGE_STAMP(2);
