@@ -71,11 +71,9 @@ struct K2Lds {
     uint64_t lmask[kK2Blocks];           // ZRL block: the non-zeros after a run of 16+ zeros
     uint32_t nzbase[kK2Blocks];          // first non-zero of each block in nz
     uint32_t recbase[kK2Blocks];         // first record of each block in the tile's records
-    uint32_t rel[kK2Blocks];             // text index of each block (relative to the key bases)
+    uint32_t acb[kK2Blocks];             // AC key base of each block: text index * 128 (Cr flag kept in bit 31)
     int dcv[kK2Blocks];                  // DC of each block
     uint8_t chroma[kK2Blocks];           // 1: a Cb / Cr block
-    uint8_t slotk[kK2Blocks];            // slot of each block in its MCU
-    uint32_t mcu[kK2Blocks];             // MCU of each block
     int prevdc[6];
     uint32_t wsum[kK2Threads / 64];
     uint32_t tot;                        // the tile's non-zeros
@@ -194,6 +192,9 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
         const int b = tid;
         const bool bact = b < nb;
         int comp = 0;
+        uint32_t rel = 0;  // the block's text index (relative to the key bases; bit 31: Cr)
+        int k = 0;         // its slot in its MCU
+        uint32_t m6 = 0;   // its MCU
         if (bact) {
             uint64_t m = lds.bmask[b];
             const uint32_t n = (uint32_t)__builtin_popcountll(m);
@@ -220,23 +221,20 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             // the block's MCU and slot, from the tile's (32-bit, small divisions)
             uint32_t kk;
             const uint32_t carry = udiv24(lds.tk[ti] + (uint32_t)(s0 + b), bpm, inv_bpm, kk);
-            const int k = (int)kk;
-            const uint32_t m6 = lds.tm6[ti] + carry;
+            k = (int)kk;
+            m6 = lds.tm6[ti] + carry;
             uint32_t mcol;
             const uint32_t mrow = lds.trow[ti] + udiv24(lds.tcol[ti] + carry, mw, inv_mw, mcol);
             comp = block_comp(k, bpm);
             // the block's text index (the Y text is in block raster order; all Cr after all Cb)
-            uint32_t rel;
             if (comp == 0) {
                 rel = (uint32_t)(((uint64_t)mrow * yv + ((uint32_t)k >> yhs)) * ybw + (uint64_t)mcol * yh +
                                  ((uint32_t)k & (yh - 1)) - ybase);
             } else {
                 rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
             }
-            lds.rel[b] = rel;
+            lds.acb[b] = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);
             lds.chroma[b] = comp != 0;
-            lds.slotk[b] = (uint8_t)k;
-            lds.mcu[b] = m6;
         }
         uint32_t T;
         const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(cnt, lds.wsum, lane, wv, T);
@@ -263,7 +261,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                     const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
                     const uint32_t zp = ((u < 4 ? regs.zlo : regs.zhi) >> (8 * (u & 3))) & 0xFF;
                     if (zp != 0 && c != 0) {
-                        const uint32_t rank = (uint32_t)__builtin_popcountll(bm & ((1ull << zp) - 1ull));
+                        const uint32_t rank = (uint32_t)__builtin_popcountll(bm << (64u - zp));  // (zp >= 1)
                         lds.nz[base + rank] = ((uint32_t)c & 0xFFFFu) | (zp << 16) | ((uint32_t)blk << 22);
                     }
                 }
@@ -282,7 +280,9 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             const int v = (int16_t)(ent & 0xFFFF);
             const int p = (int)((ent >> 16) & 63), blk = (int)(ent >> 22);
             const uint64_t m = lds.bmask[blk];
-            int run = p - (63 - __builtin_clzll((m | 1ull) & ((1ull << p) - 1ull))) - 1;
+            // zeros since the previous non-zero (or the DC): the leading zeros of the mask
+            // below p, shifted to the top (p >= 1)
+            int run = __builtin_clzll((m | 1ull) << (64 - p));
             uint32_t zb = 0;  // ZRL records of this block up to and including this entry's
             if (m & 1ull) {   // a ZRL block (rare): the long runs at or before p
                 for (uint64_t t = lds.lmask[blk] & (((1ull << p) - 1ull) | (1ull << p)); t; t &= t - 1) {
@@ -294,10 +294,10 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             run &= 15;
             const int cat = category(v);
             const int sym = (run << 4) | cat;
-            const uint32_t rel = lds.rel[blk];
+            const uint32_t acb = lds.acb[blk];
             const int tsel = lds.chroma[blk];
             atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + sym], 1u);
-            const uint32_t kk = ((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7)) + 2u * p + 1u;
+            const uint32_t kk = acb + 2u * p + 1u;
             uint32_t* kp = &lds.key[2 * tsel + 1][sym];
             if (kk < *kp) atomicMin(kp, kk);
             const uint32_t o = lds.recbase[blk] + 1 + (e - lds.nzbase[blk]) + zb;
@@ -311,17 +311,15 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
         }
         if (bact) {  // one lane per block: DC and EOB
             const uint64_t m = lds.bmask[b];
-            const uint32_t rel = lds.rel[b];
             const int tsel = comp != 0;
             const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
             // DC difference to the chain predecessor (Image.cpp:638-678)
             int pd;
             {
-                const int k = lds.slotk[b];
                 bool reset = false;
                 if (a.rst.mcus && (k == 0 || k >= (int)bpm - 2)) {
                     uint32_t r;
-                    udiv24(lds.mcu[b] + a.rst.mcu0, a.rst.mcus, inv_rst, r);
+                    udiv24(m6 + a.rst.mcu0, a.rst.mcus, inv_rst, r);
                     reset = r == 0;
                 }
                 // the predecessor (dc_pred_index): the previous Y slot, 3 blocks back for an
