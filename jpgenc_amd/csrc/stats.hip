@@ -70,10 +70,10 @@ struct K2Lds {
     uint64_t bmask[kK2Blocks];           // AC non-zero mask (bit p = zig-zag position p); bit 0: ZRL block
     uint64_t lmask[kK2Blocks];           // ZRL block: the non-zeros after a run of 16+ zeros
     uint32_t nzbase[kK2Blocks];          // first non-zero of each block in nz
-    uint32_t recbase[kK2Blocks];         // first record of each block in the tile's records
-    uint32_t acb[kK2Blocks];             // AC key base of each block: text index * 128 (Cr flag kept in bit 31)
+    // per block, read together by the symbol step: x = AC key base (text index * 128,
+    // bit 31: Cr), y = (first record - first non-zero + 1) | chroma << 31
+    uint2 binfo[kK2Blocks];
     int dcv[kK2Blocks];                  // DC of each block
-    uint8_t chroma[kK2Blocks];           // 1: a Cb / Cr block
     int prevdc[6];
     uint32_t wsum[kK2Threads / 64];
     uint32_t tot;                        // the tile's non-zeros
@@ -92,14 +92,12 @@ __device__ __forceinline__ uint32_t extra_bits(int v, int cat) {  // getCategory
 // K2 per tile, in four steps (barriers between them):
 //  A  each lane holds one natural-order row of a block: its zig-zag positions, the
 //     block's AC mask (OR over its 8 lanes), the DC;
-//  B  one lane per block: non-zeros, EOB, ZRL test (a zero run of 16 before the last
-//     non-zero: such blocks take the serial path), records; one scan gives every
-//     block's first non-zero and first record;
+//  B  one lane per block: non-zeros, EOB, ZRL test (a zero run of 16 before a later
+//     non-zero), records; one scan gives every block's first non-zero and first record;
 //  C  each row lane files its AC non-zeros into nz at their stream rank;
 //  D  one lane per non-zero (all lanes busy whatever the block's density): run
 //     (from the block mask), category, symbol, histogram, first-occurrence key, its
-//     record at recbase + 1 + rank; one lane per block: DC, EOB, and the serial
-//     blocks' AC symbols with their ZRLs.
+//     record at recbase + 1 + rank + ZRLs; one lane per block: DC and EOB.
 __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(StatsArgs a) {
     __shared__ K2Lds lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -173,7 +171,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             for (int u = 0; u < 8; ++u) {
                 const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
                 const uint32_t zp = ((u < 4 ? regs.zlo : regs.zhi) >> (8 * (u & 3))) & 0xFF;
-                m |= (uint64_t)(ok && c != 0) << zp;
+                m |= (uint64_t)(c != 0) << zp;  // (rows past the tile were loaded as zeros)
             }
             rowbits[i] = m & ~1ull;
             m |= __shfl_xor(m, 1);
@@ -233,14 +231,13 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             } else {
                 rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
             }
-            lds.acb[b] = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);
-            lds.chroma[b] = comp != 0;
         }
         uint32_t T;
         const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(cnt, lds.wsum, lane, wv, T);
         if (bact) {
             lds.nzbase[b] = ex >> 16;
-            lds.recbase[b] = rec0 + (ex & 0xFFFF);
+            lds.binfo[b] = make_uint2((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7),
+                                      (rec0 + (ex & 0xFFFF) + 1 - (ex >> 16)) | (comp ? 0x80000000u : 0u));
         }
         if (tid == 0) lds.tot = T >> 16;
         lds_barrier();
@@ -294,13 +291,14 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             run &= 15;
             const int cat = category(v);
             const int sym = (run << 4) | cat;
-            const uint32_t acb = lds.acb[blk];
-            const int tsel = lds.chroma[blk];
+            const uint2 bi = lds.binfo[blk];
+            const uint32_t acb = bi.x;
+            const int tsel = (int)(bi.y >> 31);
             atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + sym], 1u);
             const uint32_t kk = acb + 2u * p + 1u;
             uint32_t* kp = &lds.key[2 * tsel + 1][sym];
             if (kk < *kp) atomicMin(kp, kk);
-            const uint32_t o = lds.recbase[blk] + 1 + (e - lds.nzbase[blk]) + zb;
+            const uint32_t o = (bi.y & 0x7FFFFFFFu) + e + zb;  // recbase + 1 + rank + ZRLs
             if (nzr) {  // its ZRLs (F/0) just before it
                 atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + 0xF0], (uint32_t)nzr);
                 uint32_t* kz = &lds.key[2 * tsel + 1][0xF0];
@@ -335,12 +333,16 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             atomicAdd(&lds.dcnt[lane & (kHistCopies - 1)][tsel * 16 + dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
-            grec[lds.recbase[b]] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
+            // the block's first record (from LDS: keeping the scan results live through
+            // C and D costs VGPRs)
+            const uint32_t recb = (lds.binfo[b].y & 0x7FFFFFFFu) - 1u + lds.nzbase[b];
+            grec[recb] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
             if (!(m >> 63)) {  // EOB
                 atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256], 1u);
                 uint32_t* ke = &lds.key[2 * tsel + 1][0];
                 if (acb + 127u < *ke) atomicMin(ke, acb + 127u);
-                const uint32_t eo = (b + 1 < nb ? lds.recbase[b + 1] : rec0 + (T & 0xFFFF)) - 1;
+                const uint32_t eo = (b + 1 < nb ? (lds.binfo[b + 1].y & 0x7FFFFFFFu) - 1u + lds.nzbase[b + 1]
+                                                : rec0 + (T & 0xFFFF)) - 1;  // the block's last record
                 grec[eo] = rec_word(2 * tsel + 1, 0, 0);
             }
         }
