@@ -13,7 +13,7 @@ BINDIR   := jpgenc_amd/bin
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -I$(SRC) -Iinclude $(HIPEXTRA)
 CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -Wno-unused-result \
-            -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude
+            -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(SRC) -Iinclude $(HIPEXTRA)
 
 HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp coding.cpp group.cpp
 HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))

@@ -509,7 +509,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.key_y0 = s.key_y0;
     st.key_c0 = s.key_c0;
     st.key_ncb = s.key_ncb;
-    st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs_);
+    st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs());
     st.recs = s.d_recs;
     st.tcount = s.d_tcount;
     st.wgs = stats_wgs_;
@@ -539,7 +539,7 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.diag = diag_;
     e.seed = s.seed;
     e.rst = s.rst;
-    e.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs_);
+    e.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs());
     if (s.rst.mcus) {  // a stripe's first interval follows the previous stripes' ones
         e.seg_index0 = s.rst.mcu0 / s.rst.mcus;
         e.seg_markers0 = e.seg_index0 > 0 ? 1u : 0u;

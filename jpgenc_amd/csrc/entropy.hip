@@ -646,8 +646,8 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
 
 }  // namespace
 
-// Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size); about 512 in
-// all (two per CU: LDS, registers) unless overridden.  One segment (restart off):
+// Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size); about 384 in
+// all (1.5 per CU: measured best beside the other lanes) unless overridden.  One segment (restart off):
 // 128-block tiles, at least two per workgroup when the frame has two (so a
 // workgroup's stream holds >= 8 bits: its first and last 8 bits, which the
 // placement reads, are defined).  Restart intervals of R MCUs: segments of bpm*R
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override) {
     SegLayout L;
     const uint32_t nb = g.nblocks();
-    const uint32_t want = wgs_override ? wgs_override : 512u;
+    const uint32_t want = wgs_override ? wgs_override : 384u;  // (pipeline: 384 +3% over 512; 768 -12%)
     const uint64_t S = (uint64_t)g.bpm * restart_mcus;
     if (!restart_mcus || S >= nb) {
         const uint32_t nt = (nb + kK3Blocks - 1) / kK3Blocks;

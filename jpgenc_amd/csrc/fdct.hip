@@ -52,6 +52,10 @@ constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's
 #ifndef K1_STORE_AUX
 #define K1_STORE_AUX 16  // sc1: write-through coefficient stores (no dirty L2 lines at the kernel's end)
 #endif
+#ifndef K1_SHARED_CAP
+#define K1_SHARED_CAP 512  // shared-shape workgroups per launch, at most (2 per CU: measured
+                            // +1.5% in the pipeline over 1024, which filled every CU)
+#endif
 #ifndef K1_LOAD_AUX
 #define K1_LOAD_AUX 0
 #endif
@@ -590,7 +594,7 @@ uint32_t fdct_grid(const Geometry& g, bool solo) {
     const uint32_t tiles = ((g.mw + per - 1) / per) * g.mh;
     // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
     const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
-    const uint32_t cap = solo ? 256u : 1024u;
+    const uint32_t cap = solo ? 256u : (uint32_t)K1_SHARED_CAP;
     return wgs < cap ? wgs : cap;
 }
 

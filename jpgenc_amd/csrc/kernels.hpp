@@ -49,7 +49,10 @@ JPGE_HD inline int block_comp(int k, uint32_t bpm) { return k < (int)bpm - 2 ? 0
 constexpr int kHistReplicas = 8;          // spread of the global histogram atomics
 constexpr int kStatsTile = 128;           // blocks per statistics tile (4 lanes each)
 constexpr int kEntropyTile = 128;         // blocks per entropy tile (4 lanes each)
-constexpr int kEntropyMaxTilesPerWg = 4;  // tiles a persistent entropy workgroup may own
+#ifndef K3_MAX_TILES
+#define K3_MAX_TILES 4
+#endif
+constexpr int kEntropyMaxTilesPerWg = K3_MAX_TILES;  // tiles a persistent entropy workgroup may own
 constexpr int kStageBytesPerBlock = 216;  // >= worst-case 1665 bits of one block
 constexpr int kStampSlots = 16;           // diagnostic stamp words per workgroup (JPGE_STAMPS builds)
 constexpr int kEntropyRecordBytes = 48;   // per entropy workgroup: bits, edge bits, 0xFF counts
@@ -251,7 +254,7 @@ constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntr
 uint32_t fdct_grid(const Geometry& g, bool solo);
 uint32_t stats_grid(const SegLayout& L);
 // entropy partition of a frame: restart_mcus = 0 -> one segment over 128-block tiles
-// (2..kEntropyMaxTilesPerWg per workgroup, about 512 workgroups or wgs_override)
+// (2..kEntropyMaxTilesPerWg per workgroup, about 384 workgroups or wgs_override)
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override);
 inline uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) { return seg_layout(g, 0, wgs_override).grid(); }
 

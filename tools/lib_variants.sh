@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libjpge variants with extra -D flags on the HIP sources (diagnostic A/B runs):
-#   tools/lib_variants.sh name "-DFOO=1 ..." [name "flags"] ...
+#   tools/lib_variants.sh name "-DFOO=1 ..." [name "flags"] ...  (host and device sources alike)
 #   -> jpgenc_amd/lib/var/<name>/libjpge.so (use with JPGE_LIB=...)
 set -eu
 R=$(cd "$(dirname "$0")/.." && pwd)
