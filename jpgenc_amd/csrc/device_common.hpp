@@ -172,10 +172,14 @@ __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total
     static_assert(sizeof(W) == 4 && (sizeof(T) == 4 || sizeof(T) == 8), "scan word types");
     T* ws = reinterpret_cast<T*>(wsum);
     T incl = v;
+    if constexpr (sizeof(T) == 4) {
+        incl = (T)wave_scan_incl((uint32_t)v);  // DPP: no LDS permutes on the chain
+    } else {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const T o = __shfl_up(incl, d);
-        if (lane >= d) incl += o;
+        for (int d = 1; d < 64; d <<= 1) {
+            const T o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
     }
     if (kLdsSync) lds_barrier();
     else __syncthreads();
