@@ -164,6 +164,18 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
     return (uint32_t)x;
 }
 
+// OR over each aligned group of 8 lanes: DPP quad permutes for lanes 1 and 2 apart
+// (VALU only), a ds_swizzle (xor 4; no memory access) for 4 apart.
+__device__ __forceinline__ uint32_t or_lanes8(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    v |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);              // xor 4 (bitmask mode)
+    return v;
+}
+__device__ __forceinline__ uint64_t or_lanes8(uint64_t v) {
+    return ((uint64_t)or_lanes8((uint32_t)(v >> 32)) << 32) | or_lanes8((uint32_t)v);
+}
+
 // block-wide exclusive scan of one value per thread (thread order); wsum holds
 // kWaves values of T.  kLdsSync: LDS-only barriers (lds_barrier), so global loads in
 // flight stay in flight.

@@ -174,9 +174,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                 m |= (uint64_t)(c != 0) << zp;  // (rows past the tile were loaded as zeros)
             }
             rowbits[i] = m & ~1ull;
-            m |= __shfl_xor(m, 1);
-            m |= __shfl_xor(m, 2);
-            m |= __shfl_xor(m, 4);
+            m = or_lanes8(m);  // the block's 8 rows
             if (ok && row == 0) {
                 lds.bmask[blk] = m & ~1ull;
                 lds.dcv[blk] = (int16_t)(w[0] & 0xFFFF);
