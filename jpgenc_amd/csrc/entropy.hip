@@ -31,9 +31,6 @@ using namespace dev;
 #ifndef K3_WPE
 #define K3_WPE 8  // waves per SIMD: 64 VGPRs (measured: +4% in the pipeline over 4)
 #endif
-#ifndef K3_ZERO_TILE
-#define K3_ZERO_TILE 0
-#endif
 #ifndef K3_PACK_BRANCHY
 #define K3_PACK_BRANCHY 1  // (measured: the branch-free 64-bit form ran 6 us slower per 4K frame)
 #endif
@@ -99,6 +96,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
+    for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
     const int ntl = (int)wt.nt;
     if (tid < ntl) L.tcnt[tid] = a.tcount[wt.seg * a.seg.tps + wt.t0 + tid];
@@ -146,14 +144,6 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         const uint32_t nrec = __builtin_amdgcn_readfirstlane(L.tcnt[lt]);
         const uint32_t lead = wl & 31;
         uint32_t pos = lead;  // bit position in the stage
-#if K3_ZERO_TILE
-        // the whole stage zeroed once per tile (no per-round zeroing barrier)
-        for (uint32_t w = tid; w < kStageWords / 4; w += kK3Threads)
-            reinterpret_cast<uint4*>(L.stage)[w] = make_uint4(0, 0, 0, 0);
-        lds_barrier();
-#else
-        if (tid == 0) L.stage[0] = 0;
-#endif
         for (uint32_t r0 = 0; r0 < nrec; r0 += kRound) {
             const uint4 rv = nxt;
             // prefetch: the next round of this tile, else the next tile's first round
@@ -174,11 +164,6 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
             uint32_t T;
             const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true>(tl, L.wsum, lane, wv, T);
             JPGE_ACC(4, tq);
-#if !K3_ZERO_TILE
-            // zero the stage words this round reaches past the current partial word
-            for (uint32_t w = (pos >> 5) + 1 + tid; w <= ((pos + T) >> 5); w += kK3Threads) L.stage[w] = 0;
-            lds_barrier();
-#endif
             JPGE_ACC(5, tq);
             // each record into the one or two stage words it spans
             uint32_t bp = pos + ex;
@@ -225,6 +210,10 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
             if (ncw == 0) v |= L.carry;
             L.carry = v;
         }
+        // the stage words this tile used back to zero once everyone has read them (the
+        // stage starts zeroed, so the rounds OR records in without a zeroing barrier)
+        lds_barrier();
+        for (uint32_t w = tid; w <= ncw; w += kK3Threads) L.stage[w] = 0;
         wl += T;
         JPGE_ACC(2, tq);
     }
