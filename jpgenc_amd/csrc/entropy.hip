@@ -4,12 +4,13 @@
 //
 // entropy_code_kernel — G persistent workgroups; workgroup w owns the contiguous
 //   tiles [w*T/G, (w+1)*T/G) of 128 blocks (2..kEntropyMaxTilesPerWg tiles).
-//   Per tile: its symbol records (written by the statistics kernel, stream order)
-//   in rounds of 4 per thread — code bits from the tables, a workgroup scan of the
-//   bit counts, each record ORed into a big-endian word stage at its workgroup-LOCAL
-//   bit offset (the next round's records load meanwhile) — then complete words to
-//   the workgroup's private region R (the partial last word carries into the next
-//   tile).  Then the workgroup counts
+//   Its tiles' symbol records (written by the statistics kernel, stream order) form
+//   one stream, in rounds of 4 records per thread across tile boundaries — code bits
+//   from the tables, a workgroup scan of the bit counts, each record ORed into a
+//   big-endian word stage at its workgroup-LOCAL bit offset (the next round's records
+//   load meanwhile) — and complete words go to the workgroup's private region R when
+//   the stage could not take another round (the partial last word carries over).
+//   Then the workgroup counts
 //   the 0xFF bytes its stream would hold at each of the 8 byte alignments and
 //   writes a record {bits, first 8 bits, last 8 bits, ff[8]}.
 // entropy_pack_kernel — G workgroups; each scans all G records (L2-resident): bit
@@ -103,15 +104,15 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
 
-    // ---- emit every tile at workgroup-local bit offsets into R ----
-    // The tile's symbol records (K2) in rounds of 4 per thread: code bits of each,
-    // a workgroup scan of the thread totals, each thread's records ORed into the
-    // stage at its offset (every record spans at most two words).
-    uint32_t wl = 0;  // workgroup-local bit position of the current tile
+    // ---- emit the workgroup's records at workgroup-local bit offsets into R ----
+    // The symbol records (K2) in rounds of 4 per thread: code bits of each, a
+    // workgroup scan of the thread totals, each thread's records ORed into the stage at
+    // its offset (every record spans at most two words).
+    uint32_t wl = 0;  // workgroup-local bit position of the stage's first word
     // 0xFF bytes of the stream at each byte alignment, counted on the stage words as
     // they are stored (see the note after the loop).  A word's count needs the next
-    // word's first 7 bits: the last complete word of a tile waits (thread 0's `pend`)
-    // until the next tile has completed the word after it.
+    // word's first 7 bits: the last complete word of a flush waits (thread 0's `pend`)
+    // until the next flush has completed the word after it.
     uint32_t c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto count_word = [&](uint32_t x, uint32_t nx) {
         uint32_t y = x;  // bit 31-t: stream bits [32m+t, 32m+t+8) are all ones
@@ -131,71 +132,83 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * kTileRecords * 4, 0x00020000);
     constexpr uint32_t kRound = 4 * kK3Threads;  // records per round
-    auto rec_load = [&](uint32_t off_rec) -> uint4 {  // off_rec: uniform record offset, ~0u = none
-        const uint32_t off = off_rec == ~0u ? 0xFFFFFFF0u : (off_rec + 4 * tid) * 4;
+    // The workgroup's records are one stream over its tiles: tile t's count padded to a
+    // multiple of 4 (so a thread's 4 records are in one tile; the padding is never
+    // valid), rounds of kRound records run across tile boundaries, and the stage is
+    // flushed to R only when the next round might not fit (usually once, at the end).
+    lds_barrier();  // the tile counts
+    uint32_t total = 0;  // padded records of all the workgroup's tiles
+    for (int t = 0; t < ntl; ++t) total += (L.tcnt[t] + 3u) & ~3u;
+    total = __builtin_amdgcn_readfirstlane(total);
+    uint32_t cs = 0, cpre = 0;  // this thread's tile cursor (tile, its first padded index)
+    uint32_t nvalid = 0;        // valid records among the 4 prefetched
+    auto rec_load = [&](uint32_t i) -> uint4 {  // the thread's 4 records from stream index i
+        while (cs < (uint32_t)ntl) {
+            const uint32_t n = (L.tcnt[cs] + 3u) & ~3u;
+            if (i < cpre + n) break;
+            cpre += n;
+            ++cs;
+        }
+        uint32_t off = 0xFFFFFFF0u;  // (past the end: out of range, zeros)
+        nvalid = 0;
+        if (cs < (uint32_t)ntl) {
+            const uint32_t rel = i - cpre, c = L.tcnt[cs];
+            nvalid = c > rel ? min(c - rel, 4u) : 0u;
+            off = (cs * kTileRecords + rel) * 4;
+        }
         return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rec_rs, off, 0, 0));
     };
-    uint4 nxt = rec_load(0);
-    for (int lt = 0; lt < ntl; ++lt) {
-        // previous tile: stage stored, carry set; tables and tile counts in LDS
-        // (LDS-only barrier: the records in flight stay in flight)
-        lds_barrier();
-        JPGE_ACC(0, tq);
-        const uint32_t nrec = __builtin_amdgcn_readfirstlane(L.tcnt[lt]);
-        const uint32_t lead = wl & 31;
-        uint32_t pos = lead;  // bit position in the stage
-        for (uint32_t r0 = 0; r0 < nrec; r0 += kRound) {
-            const uint4 rv = nxt;
-            // prefetch: the next round of this tile, else the next tile's first round
-            const uint32_t nofs = r0 + kRound < nrec ? lt * kTileRecords + r0 + kRound
-                                  : lt + 1 < ntl      ? (lt + 1) * kTileRecords
-                                                      : ~0u;
-            nxt = rec_load(nofs);
-            const uint32_t i0 = r0 + 4 * tid;
-            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
-            uint32_t cb[4], cl[4], tl = 0;
+    constexpr uint32_t kStageBits = (kStageWords - 2) * 32;
+    constexpr uint32_t kRoundMaxBits = kRound * 32;  // (a record codes at most 16 + 11 bits)
+    static_assert(kStageBits > kRoundMaxBits, "the stage holds a round");
+    uint4 nxt = rec_load(4 * tid);
+    uint32_t lead = 0, pos = 0;  // bit position in the stage (lead: the carried partial word's bits)
+    for (uint32_t r0 = 0; r0 < total; r0 += kRound) {
+        const uint4 rv = nxt;
+        const uint32_t nv = nvalid;
+        nxt = rec_load(r0 + kRound + 4 * tid);  // the next round's (prefetch)
+        const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+        uint32_t cb[4], cl[4], tl = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t n = rec_bits(rr[q], L.tab, cb[q]);
-                cl[q] = i0 + q < nrec ? n : 0u;
-                tl += cl[q];
-            }
-            JPGE_ACC(3, tq);
-            uint32_t T;
-            const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true>(tl, L.wsum, lane, wv, T);
-            JPGE_ACC(4, tq);
-            JPGE_ACC(5, tq);
-            // each record into the one or two stage words it spans
-            uint32_t bp = pos + ex;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-#if K3_PACK_BRANCHY
-                if (cl[q]) {
-                    const uint32_t sh = bp & 31, n = cl[q];
-                    const uint32_t v = cb[q] << (32 - n);  // MSB-aligned (n >= 1)
-                    atomicOr(&L.stage[bp >> 5], v >> sh);
-                    if (sh + n > 32) atomicOr(&L.stage[(bp >> 5) + 1], v << (32 - sh));
-                    bp += n;
-                }
-#else
-                const uint32_t n = cl[q], sh = bp & 31;
-                const uint64_t v = n ? ((uint64_t)cb[q] << (64 - n)) >> sh : 0ull;  // MSB-aligned at bp
-                atomicOr(&L.stage[bp >> 5], (uint32_t)(v >> 32));
-                if ((uint32_t)v) atomicOr(&L.stage[(bp >> 5) + 1], (uint32_t)v);
-                bp += n;
-#endif
-            }
-            pos += T;
-            lds_barrier();
-            JPGE_ACC(6, tq);
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t n = rec_bits(rr[q], L.tab, cb[q]);
+            cl[q] = (uint32_t)q < nv ? n : 0u;
+            tl += cl[q];
         }
-        const uint32_t T = pos - lead;  // this tile's bits
-        const uint32_t ncw = pos >> 5;  // complete words of the tile stream
-        JPGE_ACC(1, tq);
+        JPGE_ACC(3, tq);
+        uint32_t T;
+        const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true>(tl, L.wsum, lane, wv, T);
+        JPGE_ACC(4, tq);
+        // each record into the one or two stage words it spans
+        uint32_t bp = pos + ex;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#if K3_PACK_BRANCHY
+            if (cl[q]) {
+                const uint32_t sh = bp & 31, n = cl[q];
+                const uint32_t v = cb[q] << (32 - n);  // MSB-aligned (n >= 1)
+                atomicOr(&L.stage[bp >> 5], v >> sh);
+                if (sh + n > 32) atomicOr(&L.stage[(bp >> 5) + 1], v << (32 - sh));
+                bp += n;
+            }
+#else
+            const uint32_t n = cl[q], sh = bp & 31;
+            const uint64_t v = n ? ((uint64_t)cb[q] << (64 - n)) >> sh : 0ull;  // MSB-aligned at bp
+            atomicOr(&L.stage[bp >> 5], (uint32_t)(v >> 32));
+            if ((uint32_t)v) atomicOr(&L.stage[(bp >> 5) + 1], (uint32_t)v);
+            bp += n;
+#endif
+        }
+        pos += T;
+        lds_barrier();
+        JPGE_ACC(6, tq);
+        if (r0 + kRound < total && pos + kRoundMaxBits <= kStageBits) continue;
+        // ---- flush: complete words to R, the partial word carried ----
+        const uint32_t ncw = pos >> 5;  // complete words in the stage
         const uint32_t wbase = wl >> 5;
         for (uint32_t w = tid; w < ncw; w += kK3Threads) {
             uint32_t v = L.stage[w];
-            if (w == 0) v |= L.carry;  // partial last word of the previous tile
+            if (w == 0) v |= L.carry;  // partial last word of the previous flush
             R32[wbase + w] = __builtin_bswap32(v);
             if (w + 1 < ncw) count_word(v, L.stage[w + 1]);
         }
@@ -210,11 +223,14 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
             if (ncw == 0) v |= L.carry;
             L.carry = v;
         }
-        // the stage words this tile used back to zero once everyone has read them (the
-        // stage starts zeroed, so the rounds OR records in without a zeroing barrier)
+        // the stage words used back to zero once everyone has read them (the stage
+        // starts zeroed, so the rounds OR records in without a zeroing barrier)
         lds_barrier();
         for (uint32_t w = tid; w <= ncw; w += kK3Threads) L.stage[w] = 0;
-        wl += T;
+        lds_barrier();
+        wl += pos - lead;
+        lead = wl & 31;
+        pos = lead;
         JPGE_ACC(2, tq);
     }
     const uint32_t Lb = wl;  // this workgroup's bits (>= 6: every block codes >= 2 bits, >= 3 blocks)
