@@ -71,6 +71,14 @@ __device__ __forceinline__ int category(int v) {
     return av ? 32 - __builtin_clz((unsigned)av) : 0;
 }
 
+// Symbol record words (kernels.hpp): table << 24 | symbol << 16 | extra bits.
+__device__ __forceinline__ uint32_t rec_word(uint32_t table, uint32_t sym, uint32_t bits) {
+    return (table << 24) | (sym << 16) | bits;
+}
+__device__ __forceinline__ uint32_t extra_bits(int v, int cat) {  // getCategoryAndCode, Coding.hpp:214-221
+    return (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1);
+}
+
 constexpr int kPartsPerBlock = 4;  // lanes cooperating on one block's non-zero coefficients
 
 // DC predecessor of flat block g (Image.cpp:638-678): the Y chain runs in MCU
@@ -143,6 +151,11 @@ __device__ __forceinline__ void export_hist(const HistPtrs& h, uint32_t* host_cn
         for (int r = 0; r < kHistReplicas; ++r) c += h.cnt[r * 1024 + t];
         host_cnt[t] = c;
         host_key[t] = h.key[t];
+        // read: back to zero for the slot's next frame (a fused K1 cannot zero them
+        // itself: its workgroups flush while others may not have started)
+#pragma unroll
+        for (int r = 0; r < kHistReplicas; ++r) h.cnt[r * 1024 + t] = 0;
+        h.key[t] = 0;
     }
     __syncthreads();
     if (tid == 0) {

@@ -218,7 +218,12 @@ struct Encoder::Slot {
     size_t cap_ubuf = 0;
     uint32_t* d_recs = nullptr;    // K2's symbol records, kTileRecords per entropy tile
     uint32_t* d_tcount = nullptr;  // records per tile
-    size_t cap_tiles = 0;
+    size_t cap_tiles = 0;          // (capacities: records, in words; tiles)
+    size_t cap_recs = 0;
+    FusedTileInfo* d_tinfo = nullptr;  // fused K1: per K1 tile, the DC fix-up's inputs
+    size_t cap_tinfo = 0;
+    bool fused = false;            // this frame runs the fused K1 (+ DC fix-up) instead of K1 + K2
+    bool hist_clean = false;       // the histogram replicas are zero (allocation, or exported since)
     uint8_t* d_out = nullptr;
     uint32_t* d_tab = nullptr;  // [1024] tables, then the header bytes (one upload)
     // pinned host staging
@@ -252,7 +257,7 @@ struct Encoder::Slot {
 
     ~Slot() {
         hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
-        hipFree(d_recs); hipFree(d_tcount);
+        hipFree(d_recs); hipFree(d_tcount); hipFree(d_tinfo);
         hipFree(d_out); hipFree(d_tab);
         hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_result);
         for (auto& e : ev) if (e) hipEventDestroy(e);
@@ -354,6 +359,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
     if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     if (const char* sw = std::getenv("JPGE_STATS_WGS")) e->stats_wgs_ = (uint32_t)std::strtoul(sw, nullptr, 10);
+    if (const char* fu = std::getenv("JPGE_FUSED")) e->fused_ = std::strtoul(fu, nullptr, 10) != 0;
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
@@ -441,16 +447,21 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         JPGE_HIP(hipMalloc((void**)&s.d_coef, nblk * 128));
         s.cap_blk = nblk;
     }
-    const CtlLayout L(layout(g).grid());
-    const size_t ntiles = seg_tiles(layout(g));
-    if (ntiles > s.cap_tiles) {
-        hipFree(s.d_recs); hipFree(s.d_tcount);
-        s.d_recs = nullptr; s.d_tcount = nullptr; s.cap_tiles = 0;
-        JPGE_HIP(hipMalloc((void**)&s.d_recs, ntiles * kTileRecords * 4));
+    // (sized for the K2 layout and the fused one alike: a slot may run either)
+    const SegLayout fl = fused_layout(g, entropy_wgs());
+    const CtlLayout L(std::max(layout(g).grid(), fl.grid()));
+    const size_t ntiles = std::max<size_t>(seg_tiles(layout(g)), fused_tiles(g));
+    const size_t nrecs = std::max<size_t>((size_t)seg_tiles(layout(g)) * kTileRecords, (size_t)fused_tiles(g) * kFusedSlotRecs);
+    if (ntiles > s.cap_tiles || nrecs > s.cap_recs) {
+        hipFree(s.d_recs); hipFree(s.d_tcount); hipFree(s.d_tinfo);
+        s.d_recs = nullptr; s.d_tcount = nullptr; s.d_tinfo = nullptr; s.cap_tiles = s.cap_recs = 0;
+        JPGE_HIP(hipMalloc((void**)&s.d_recs, nrecs * 4));
         JPGE_HIP(hipMalloc((void**)&s.d_tcount, ntiles * 4));
+        JPGE_HIP(hipMalloc((void**)&s.d_tinfo, ntiles * sizeof(FusedTileInfo)));
         s.cap_tiles = ntiles;
+        s.cap_recs = nrecs;
     }
-    const size_t ubuf = entropy_ubuf_bytes(layout(g));
+    const size_t ubuf = std::max(entropy_ubuf_bytes(layout(g)), entropy_ubuf_bytes(fl));
     if (ubuf > s.cap_ubuf) {
         hipFree(s.d_ubuf); s.d_ubuf = nullptr; s.cap_ubuf = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_ubuf, ubuf));
@@ -459,7 +470,9 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     if (L.alloc > s.cap_ctl) {
         hipFree(s.d_ctl); s.d_ctl = nullptr; s.cap_ctl = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_ctl, L.alloc));
+        JPGE_HIP(hipMemset(s.d_ctl, 0, L.alloc));
         s.cap_ctl = L.alloc;
+        s.hist_clean = true;
     }
     if (in_bytes > s.cap_in) {
         hipFree(s.d_in); s.d_in = nullptr; s.cap_in = 0;
@@ -474,9 +487,13 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     return kOk;
 }
 
+SegLayout Encoder::slot_layout(const Slot& s) const {
+    return s.fused ? fused_layout(s.g, entropy_wgs()) : seg_layout(s.g, s.rst.mcus, entropy_wgs());
+}
+
 // Kernel parameter blocks of a slot's frame (or stripe).
 FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
-    const CtlLayout L(layout(s.g).grid());
+    const CtlLayout L(slot_layout(s).grid());
     FdctArgs a;
     a.rgb = s.in_dev;
     a.stride = s.in_stride;
@@ -493,12 +510,21 @@ FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
     a.imp_src = imp ? reinterpret_cast<const uint4*>(imp->d_tab_host) : nullptr;
     a.imp_dst = imp ? reinterpret_cast<uint4*>(imp->d_tab) : nullptr;
     a.imp_n16 = imp ? (uint32_t)((kTabBytes + imp->hdr_len + 15) / 16) : 0u;
+    if (s.fused) {  // symbols instead of coefficients; the histograms are already zero
+        a.fused = true;
+        a.recs = s.d_recs;
+        a.tcount = s.d_tcount;
+        a.tinfo = s.d_tinfo;
+        a.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
+        a.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
+        a.zero_words = 0;
+    }
     a.dbg = d_dbg_;
     return a;
 }
 
 StatsArgs Encoder::stats_args(Slot& s) {
-    const CtlLayout L(layout(s.g).grid());
+    const CtlLayout L(slot_layout(s).grid());
     StatsArgs st;
     st.coef = s.d_coef;
     st.g = s.g;
@@ -518,7 +544,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
 }
 
 EntropyArgs Encoder::entropy_args(Slot& s) {
-    const CtlLayout L(layout(s.g).grid());
+    const CtlLayout L(slot_layout(s).grid());
     EntropyArgs e;
     e.coef = s.d_coef;
     e.recs = s.d_recs;
@@ -539,7 +565,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.diag = diag_;
     e.seed = s.seed;
     e.rst = s.rst;
-    e.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs());
+    e.seg = slot_layout(s);
+    e.slot_words = s.fused ? (uint32_t)kFusedSlotRecs : 0u;
     if (s.rst.mcus) {  // a stripe's first interval follows the previous stripes' ones
         e.seg_index0 = s.rst.mcu0 / s.rst.mcus;
         e.seg_markers0 = e.seg_index0 > 0 ? 1u : 0u;
@@ -596,6 +623,13 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.key_y0 = s.key_c0 = s.key_ncb = 0;
     s.img_w = f.width;
     s.img_h = f.height;
+    // the fused K1 (symbols straight from the transform) for pipelined 4:2:0 frames
+    s.fused = fused_ && lanes_.size() > 1 && !s.rst.mcus && !g.row8() && g.bpm == 6 && !(flags & kFlagCoefficients);
+    if (s.fused && !s.hist_clean) {  // (a previous frame of the slot never exported: zero them)
+        const CtlLayout Lc(slot_layout(s).grid());
+        JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, Lc.rec, s.stream));
+    }
+    s.hist_clean = false;
     const FdctArgs a = fdct_args(s, f.maxval, imp);
     const StatsArgs st2 = stats_args(s);
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
@@ -604,7 +638,18 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
     JPGE_HIP(launch_fdct(a, s.stream));
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
-    JPGE_HIP(launch_stats(st2, s.stream));
+    if (s.fused) {
+        FixupArgs fx;
+        fx.tinfo = s.d_tinfo;
+        fx.recs = s.d_recs;
+        fx.g = g;
+        fx.ntiles = fused_tiles(g);
+        fx.tiles_per_row = (g.mw + kFusedTileMcus - 1) / kFusedTileMcus;
+        fx.hist = a.hist;
+        JPGE_HIP(launch_dc_fixup(fx, s.stream));
+    } else {
+        JPGE_HIP(launch_stats(st2, s.stream));
+    }
     if (s.timed) JPGE_HIP(hipEventRecord(s.ev[2], s.stream));
     s.seq = ++seq_counter_;
     s.hist = st2.hist;
@@ -613,6 +658,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
                                     s.stream));
         s.export_queued.store(1, std::memory_order_release);
+        s.hist_clean = true;
     }
     return kOk;
 }
@@ -866,6 +912,7 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
             note(j, st);
             if (!st && si) {  // exported by frame j's code kernel
                 si->export_queued.store(1, std::memory_order_release);
+                si->hist_clean = true;
                 si = nullptr;
             }
         }
@@ -874,7 +921,10 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
             const hipError_t e = launch_hist_export(si->hist, si->d_hist_host->cnt, si->d_hist_host->key,
                                                     &si->d_hist_host->seq, si->seq, si->stream);
             note(i, e == hipSuccess ? kOk : kErrHip);
-            if (e == hipSuccess) si->export_queued.store(1, std::memory_order_release);
+            if (e == hipSuccess) {
+                si->export_queued.store(1, std::memory_order_release);
+                si->hist_clean = true;
+            }
         }
         if (k >= 0 && k < n) {
             Slot& s = *ln.slots[k % S];
@@ -911,7 +961,7 @@ int Encoder::fdct_quant(const FrameDesc& f, const uint8_t qy[64], const uint8_t 
     std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
-    int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput, nullptr, true);
+    int st = phase1(s, f, qy, qc, flags | kFlagDeviceOutput | kFlagCoefficients, nullptr, true);
     if (st) { hipStreamSynchronize(s.stream); return st; }
     JPGE_HIP(hipStreamSynchronize(s.stream));
     const Geometry& g = s.g;
@@ -984,6 +1034,7 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
     s.rst = Restart();
     s.rst.mcus = restart_mcus_;
     s.rst.mcu0 = d.mcu_row0 * g.mw;
+    s.fused = false;
     s.key_y0 = 2ull * d.mcu_row0 * (2ull * g.mw);  // Y blocks above the stripe (raster)
     s.key_c0 = (uint64_t)d.mcu_row0 * g.mw;         // Cb blocks above it
     s.key_ncb = (uint64_t)mh_img * g.mw;            // Cb blocks of the image
@@ -1391,6 +1442,7 @@ int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_
     s.export_queued.store(0, std::memory_order_relaxed);
     // applyDCT(Arai) + applyQuantization (Image.cpp:844-871) into the MCU layout; the
     // control block is zeroed here (K1 does it on the RGB8 path)
+    s.fused = false;
     const CtlLayout L(layout(g).grid());
     JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, L.total, st));
     PlaneBlockArgs b{};
@@ -1413,6 +1465,7 @@ int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_
     s.hist = st2.hist;
     JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq, st));
     s.export_queued.store(1, std::memory_order_release);
+    s.hist_clean = true;
     FrameDesc f;
     f.out = out;
     f.cap = cap;

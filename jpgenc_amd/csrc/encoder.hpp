@@ -22,6 +22,7 @@ namespace jpge {
 
 constexpr uint32_t kFlagDeviceInput = 1u;
 constexpr uint32_t kFlagDeviceOutput = 2u;
+constexpr uint32_t kFlagCoefficients = 1u << 30;  // (internal) the frame's coefficients are read back: no fused K1
 
 struct FrameDesc {
     const uint8_t* rgb = nullptr;
@@ -149,12 +150,15 @@ class Encoder {
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
+    bool fused_ = false;        // JPGE_FUSED=1: the fused K1 (+ DC fix-up) for pipelined 4:2:0 frames (measured slower)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
     int mode_ = 420;            // subsampling mode (jpge_set_subsampling)
     // entropy workgroups: the override, else 512 for a single lane (its frames' latency:
     // -5 us at 4K) and seg_layout's default (384) beside other lanes (+3% throughput)
     uint32_t entropy_wgs() const { return entropy_wgs_ ? entropy_wgs_ : (lanes_.size() == 1 ? 512u : 0u); }
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
+    // the entropy partition a slot's current frame runs on (fused K1 frames: K1's tiles)
+    SegLayout slot_layout(const Slot& s) const;
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain

@@ -39,6 +39,7 @@ constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
 constexpr int kMaxTiles = kEntropyMaxTilesPerWg;
+constexpr int kTcntSlots = kFusedTilesPerWg > kMaxTiles ? kFusedTilesPerWg : kMaxTiles;  // tiles of a workgroup, any layout
 constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-case tile + lead
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
@@ -58,7 +59,7 @@ static_assert(sizeof(WgRecord) == kEntropyRecordBytes, "record size");
 struct K3Lds {
     uint32_t stage[kStageWords];  // the tile's big-endian bit stream
     uint32_t tab[4 * 256];        // (len << 16) | code
-    uint32_t tcnt[kMaxTiles];     // symbol records of each of the workgroup's tiles
+    uint32_t tcnt[kTcntSlots];    // symbol records of each of the workgroup's tiles
     uint32_t wsum[kK3Waves];
     uint32_t cnt8[8];
     uint32_t carry;
@@ -129,8 +130,9 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     // zeros), so no branch merges in-flight registers and the in-order wait for a
     // round's records never waits for the prefetch behind it.
     const uint32_t gt0 = wt.seg * a.seg.tps + wt.t0;  // global number of the first tile
+    const uint32_t slot = a.slot_words ? a.slot_words : (uint32_t)kTileRecords;  // record words per tile
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * kTileRecords * 4, 0x00020000);
+        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * slot), 0, ntl * slot * 4, 0x00020000);
     constexpr uint32_t kRound = 4 * kK3Threads;  // records per round
     // The workgroup's records are one stream over its tiles: tile t's count padded to a
     // multiple of 4 (so a thread's 4 records are in one tile; the padding is never
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         if (cs < (uint32_t)ntl) {
             const uint32_t rel = i - cpre, c = L.tcnt[cs];
             nvalid = c > rel ? min(c - rel, 4u) : 0u;
-            off = (cs * kTileRecords + rel) * 4;
+            off = (cs * slot + rel) * 4;
         }
         return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rec_rs, off, 0, 0));
     };
@@ -687,6 +689,20 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
     };
     part(L.sblk, L.tps, L.wps);
     part(L.lblk, L.ltps, L.lwps);
+    return L;
+}
+
+SegLayout fused_layout(const Geometry& g, uint32_t wgs_override) {
+    SegLayout L;
+    const uint32_t nt = fused_tiles(g);
+    const uint32_t want = wgs_override ? wgs_override : 384u;
+    const uint32_t lo = (nt + kFusedTilesPerWg - 1) / kFusedTilesPerWg;
+    // (a tile of one MCU codes >= 12 bits: every workgroup's stream has its 8 edge bits)
+    const uint32_t G = want < lo ? lo : (want > nt ? nt : want);
+    L.nseg = 1;
+    L.sblk = L.lblk = g.nblocks();
+    L.tps = L.ltps = nt;
+    L.wps = L.lwps = G;
     return L;
 }
 
