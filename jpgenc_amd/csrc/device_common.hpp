@@ -151,11 +151,6 @@ __device__ __forceinline__ void export_hist(const HistPtrs& h, uint32_t* host_cn
         for (int r = 0; r < kHistReplicas; ++r) c += h.cnt[r * 1024 + t];
         host_cnt[t] = c;
         host_key[t] = h.key[t];
-        // read: back to zero for the slot's next frame (a fused K1 cannot zero them
-        // itself: its workgroups flush while others may not have started)
-#pragma unroll
-        for (int r = 0; r < kHistReplicas; ++r) h.cnt[r * 1024 + t] = 0;
-        h.key[t] = 0;
     }
     __syncthreads();
     if (tid == 0) {

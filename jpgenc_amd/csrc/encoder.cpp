@@ -78,6 +78,8 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto next_query = t0 + std::chrono::milliseconds(2);
+    clk::time_point idle_since{};  // the stream was first seen idle without the word
+    bool idle = false;
     for (uint32_t spins = 0;; ++spins) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return kOk;
         if (nap) std::this_thread::sleep_for(std::chrono::microseconds(10));
@@ -87,9 +89,23 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool
         next_query = now + std::chrono::milliseconds(1);
         const hipError_t q = hipStreamQuery(stream);
         if (q != hipSuccess && q != hipErrorNotReady) return kErrHip;
+        // An idle stream without the word: its writer never ran (an error), or the
+        // word is still on its way to host memory (seen with several processes on one
+        // GPU): an error only once it stays missing for 200 ms.
         if (q == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq &&
-            (!queued || queued->load(std::memory_order_acquire)))
-            return kErrInternal;
+            (!queued || queued->load(std::memory_order_acquire))) {
+            if (!idle) {
+                idle = true;
+                idle_since = now;
+            } else if (now - idle_since > std::chrono::milliseconds(200)) {
+                if (std::getenv("JPGE_DEBUG")) std::fprintf(stderr, "jpge: wait_seq: word %llu != %llu, stream idle\n",
+                                                          (unsigned long long)__atomic_load_n(word, __ATOMIC_ACQUIRE),
+                                                          (unsigned long long)seq);
+                return kErrInternal;
+            }
+        } else {
+            idle = false;
+        }
         if (now - t0 > std::chrono::seconds(20)) return kErrTimeout;
     }
 }
@@ -223,7 +239,6 @@ struct Encoder::Slot {
     FusedTileInfo* d_tinfo = nullptr;  // fused K1: per K1 tile, the DC fix-up's inputs
     size_t cap_tinfo = 0;
     bool fused = false;            // this frame runs the fused K1 (+ DC fix-up) instead of K1 + K2
-    bool hist_clean = false;       // the histogram replicas are zero (allocation, or exported since)
     uint8_t* d_out = nullptr;
     uint32_t* d_tab = nullptr;  // [1024] tables, then the header bytes (one upload)
     // pinned host staging
@@ -470,9 +485,7 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     if (L.alloc > s.cap_ctl) {
         hipFree(s.d_ctl); s.d_ctl = nullptr; s.cap_ctl = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_ctl, L.alloc));
-        JPGE_HIP(hipMemset(s.d_ctl, 0, L.alloc));
         s.cap_ctl = L.alloc;
-        s.hist_clean = true;
     }
     if (in_bytes > s.cap_in) {
         hipFree(s.d_in); s.d_in = nullptr; s.cap_in = 0;
@@ -625,11 +638,10 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.img_h = f.height;
     // the fused K1 (symbols straight from the transform) for pipelined 4:2:0 frames
     s.fused = fused_ && lanes_.size() > 1 && !s.rst.mcus && !g.row8() && g.bpm == 6 && !(flags & kFlagCoefficients);
-    if (s.fused && !s.hist_clean) {  // (a previous frame of the slot never exported: zero them)
+    if (s.fused) {  // (a fused K1 cannot zero them itself: its workgroups flush while others may not have started)
         const CtlLayout Lc(slot_layout(s).grid());
         JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, Lc.rec, s.stream));
     }
-    s.hist_clean = false;
     const FdctArgs a = fdct_args(s, f.maxval, imp);
     const StatsArgs st2 = stats_args(s);
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
@@ -658,7 +670,6 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
                                     s.stream));
         s.export_queued.store(1, std::memory_order_release);
-        s.hist_clean = true;
     }
     return kOk;
 }
@@ -693,7 +704,18 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     uint64_t nsym = 0;
     for (int i = 0; i < 1024; ++i) nsym += cnt_all[i];
     s.symbols = nsym;
-    if (bad) return kErrInternal;
+    if (bad) {
+        if (std::getenv("JPGE_DEBUG")) {
+            std::fprintf(stderr, "jpge: table build failed (seq %llu):", (unsigned long long)s.seq);
+            for (int t = 0; t < 4; ++t) {
+                uint64_t n = 0;
+                for (int i = 0; i < 256; ++i) n += cnt_all[t * 256 + i];
+                std::fprintf(stderr, " t%d ok=%d n=%llu", t, ok[t], (unsigned long long)n);
+            }
+            std::fprintf(stderr, "\n");
+        }
+        return kErrInternal;
+    }
     const HuffTable* tp[4] = {&tabs[0], &tabs[1], &tabs[2], &tabs[3]};
     const std::vector<uint8_t> hdr = jfif_headers(s.img_w, s.img_h, s.qy, s.qc, tp, restart_mcus_,
                                                     (uint8_t)((s.g.yh << 4) | s.g.yv()));
@@ -912,7 +934,6 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
             note(j, st);
             if (!st && si) {  // exported by frame j's code kernel
                 si->export_queued.store(1, std::memory_order_release);
-                si->hist_clean = true;
                 si = nullptr;
             }
         }
@@ -921,10 +942,7 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
             const hipError_t e = launch_hist_export(si->hist, si->d_hist_host->cnt, si->d_hist_host->key,
                                                     &si->d_hist_host->seq, si->seq, si->stream);
             note(i, e == hipSuccess ? kOk : kErrHip);
-            if (e == hipSuccess) {
-                si->export_queued.store(1, std::memory_order_release);
-                si->hist_clean = true;
-            }
+            if (e == hipSuccess) si->export_queued.store(1, std::memory_order_release);
         }
         if (k >= 0 && k < n) {
             Slot& s = *ln.slots[k % S];
@@ -1465,7 +1483,6 @@ int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_
     s.hist = st2.hist;
     JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq, st));
     s.export_queued.store(1, std::memory_order_release);
-    s.hist_clean = true;
     FrameDesc f;
     f.out = out;
     f.cap = cap;
