@@ -3,7 +3,7 @@
 //
 // One wavefront owns a tile of 4 MCUs (64x16 px) staged in LDS for the column
 // pass, the transpose and the row pass; each lane stores one 16-byte row of a
-// block straight from registers.  One persistent 16-wave workgroup per CU owns a
+// block straight from registers.  Persistent workgroups (8 waves, two per CU, alone) own a
 // contiguous run of tiles; its waves take tiles from an LDS counter (the SIMD
 // favours its oldest wave, so static shares finish unevenly) and prefetch the next
 // tile's RGB run during the transform.  Three rounds per tile (chroma, Y MCUs 0-1,
@@ -62,11 +62,15 @@ constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's
 #define K1_LOAD_AUX 0
 #endif
 
-// Workgroup shapes: 16 waves = one workgroup per CU (4 waves per SIMD), whose
+// Workgroup shapes: solo, 8 waves = two workgroups per CU (4 waves per SIMD), whose
 // waves balance their tiles among themselves — best when the kernel has the GPU to
-// itself; 4 waves = four workgroups per CU, which co-schedule beside other lanes'
-// kernels (a whole-CU workgroup waits for a whole CU to drain).
-constexpr int kK1WavesSolo = 16, kK1WavesShared = 4;
+// itself (one 16-wave workgroup per CU ran 3% slower, 4- or 2-wave ones 2%); shared,
+// 4 waves, at most two per CU, which co-schedule beside other lanes' kernels (a
+// whole-CU workgroup waits for a whole CU to drain).
+#ifndef K1_WAVES_SOLO
+#define K1_WAVES_SOLO 8  // solo shape: two 8-wave workgroups per CU (3% faster alone than one of 16)
+#endif
+constexpr int kK1WavesSolo = K1_WAVES_SOLO, kK1WavesShared = 4;
 constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
 constexpr int kTmpBlock = 72;    // doubles per transpose block (rows of 9 doubles)
 constexpr int kTmpRow = 9;
@@ -841,7 +845,7 @@ uint32_t fdct_grid(const Geometry& g, bool solo) {
     const uint32_t tiles = ((g.mw + per - 1) / per) * g.mh;
     // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
     const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
-    const uint32_t cap = solo ? 256u : (uint32_t)K1_SHARED_CAP;
+    const uint32_t cap = solo ? 256u * (16u / (uint32_t)kK1WavesSolo) : (uint32_t)K1_SHARED_CAP;
     return wgs < cap ? wgs : cap;
 }
 
