@@ -272,16 +272,28 @@ def thread_cpu() -> dict:
 
 
 def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
-    """Per-launch HBM bytes per stage from the newest committed rocprofv3 PMC summary
-    (profiles/pmc_rNN.json; the entropy stage = its code, placement-scan and pack kernels)."""
+    """Per-launch HBM bytes per stage from the newest committed rocprofv3 PMC summary of this
+    frame size (profiles/pmc_rNN.json for 4K, profiles/rNN_pmc_<size>.json for others; the
+    entropy stage = its code, placement-scan and pack kernels)."""
+    def round_of(f):
+        return f[5:7] if f.startswith("pmc_r") else f[1:3]
     try:
-        names = sorted(f for f in os.listdir(profile_dir) if f.startswith("pmc_r") and f.endswith(".json"))
-        with open(os.path.join(profile_dir, names[-1])) as f:
-            d = json.load(f)
-        if d.get("width") != width or d.get("height") != height:
-            return {}
-        per = {k.split("<")[0]: v["hbm_bytes_per_launch"] for k, v in d["kernels"].items()}
-    except (OSError, ValueError, KeyError, IndexError):
+        names = sorted((f for f in os.listdir(profile_dir) if f.endswith(".json") and
+                        (f.startswith("pmc_r") or (f.startswith("r") and "_pmc_" in f))),
+                       key=round_of, reverse=True)
+    except OSError:
+        return {}
+    per = None
+    for name in names:
+        try:
+            with open(os.path.join(profile_dir, name)) as f:
+                d = json.load(f)
+            if d.get("width") == width and d.get("height") == height:
+                per = {k.split("<")[0]: v["hbm_bytes_per_launch"] for k, v in d["kernels"].items()}
+                break
+        except (OSError, ValueError, KeyError, TypeError):
+            continue
+    if per is None:
         return {}
     out = {k: v for k, v in per.items() if not k.startswith("entropy_")}
     ent = [v for k, v in per.items() if k.startswith("entropy_")]

@@ -62,13 +62,13 @@ constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's
 #define K1_LOAD_AUX 0
 #endif
 
-// Workgroup shapes: solo, 8 waves = two workgroups per CU (4 waves per SIMD), whose
+// Workgroup shapes: solo, one 16-wave workgroup per CU (4 waves per SIMD), whose
 // waves balance their tiles among themselves — best when the kernel has the GPU to
-// itself (one 16-wave workgroup per CU ran 3% slower, 4- or 2-wave ones 2%); shared,
+// itself (two 8-wave workgroups per CU: equal at 4K, 4% slower at 16384^2); shared,
 // 4 waves, at most two per CU, which co-schedule beside other lanes' kernels (a
 // whole-CU workgroup waits for a whole CU to drain).
 #ifndef K1_WAVES_SOLO
-#define K1_WAVES_SOLO 8  // solo shape: two 8-wave workgroups per CU (3% faster alone than one of 16)
+#define K1_WAVES_SOLO 16
 #endif
 constexpr int kK1WavesSolo = K1_WAVES_SOLO, kK1WavesShared = 4;
 constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
