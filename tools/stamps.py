@@ -10,7 +10,7 @@ SLOTS = 16
 KERNELS = ["fdct", "stats", "entropy_code", "entropy_pack"]
 PHASES = {
     "fdct": ["start", "", "", "", "", "", "", "end"],
-    "stats": ["start", "staged", "histogram", "flush", "", "", "", ""],
+    "stats": ["start", "", "tiles", "flush", "", "", "", ""],
     "entropy_code": ["start", "emit", "count8", "", "", "", "", ""],
     "entropy_pack": ["start", "scan", "output", "", "", "", "", ""],
 }
