@@ -186,8 +186,9 @@ __device__ __forceinline__ uint64_t or_lanes8(uint64_t v) {
 
 // block-wide exclusive scan of one value per thread (thread order); wsum holds
 // kWaves values of T.  kLdsSync: LDS-only barriers (lds_barrier), so global loads in
-// flight stay in flight.
-template <int kWaves, typename T, typename W, bool kLdsSync = false>
+// flight stay in flight.  kLead: a barrier before wsum is written, for callers whose
+// previous reads of wsum are not already behind one (without it: one barrier).
+template <int kWaves, typename T, typename W, bool kLdsSync = false, bool kLead = true>
 __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total) {
     static_assert(sizeof(W) == 4 && (sizeof(T) == 4 || sizeof(T) == 8), "scan word types");
     T* ws = reinterpret_cast<T*>(wsum);
@@ -201,8 +202,10 @@ __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total
             if (lane >= d) incl += o;
         }
     }
-    if (kLdsSync) lds_barrier();
-    else __syncthreads();
+    if constexpr (kLead) {
+        if (kLdsSync) lds_barrier();
+        else __syncthreads();
+    }
     if (lane == 63) ws[wv] = incl;
     if (kLdsSync) lds_barrier();
     else __syncthreads();

@@ -60,7 +60,7 @@ struct K3Lds {
     uint32_t stage[kStageWords];  // the tile's big-endian bit stream
     uint32_t tab[4 * 256];        // (len << 16) | code
     uint32_t tcnt[kTcntSlots];    // symbol records of each of the workgroup's tiles
-    uint32_t wsum[kK3Waves];
+    uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds)
     uint32_t cnt8[8];
     uint32_t carry;
 };
@@ -165,6 +165,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     static_assert(kStageBits > kRoundMaxBits, "the stage holds a round");
     uint4 nxt = rec_load(4 * tid);
     uint32_t lead = 0, pos = 0;  // bit position in the stage (lead: the carried partial word's bits)
+    uint32_t par = 0;            // scan buffer of this round
     for (uint32_t r0 = 0; r0 < total; r0 += kRound) {
         const uint4 rv = nxt;
         const uint32_t nv = nvalid;
@@ -179,7 +180,10 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         }
         JPGE_ACC(3, tq);
         uint32_t T;
-        const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true>(tl, L.wsum, lane, wv, T);
+        // (the one barrier of a round: wsum alternates, so no wave can overwrite a total
+        // another still reads, and the stage ORs of consecutive rounds commute)
+        const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true, false>(tl, L.wsum[par], lane, wv, T);
+        par ^= 1u;
         JPGE_ACC(4, tq);
         // each record into the one or two stage words it spans
         uint32_t bp = pos + ex;
@@ -202,10 +206,10 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
 #endif
         }
         pos += T;
-        lds_barrier();
         JPGE_ACC(6, tq);
         if (r0 + kRound < total && pos + kRoundMaxBits <= kStageBits) continue;
         // ---- flush: complete words to R, the partial word carried ----
+        lds_barrier();  // every record of the stage ORed in
         const uint32_t ncw = pos >> 5;  // complete words in the stage
         const uint32_t wbase = wl >> 5;
         for (uint32_t w = tid; w < ncw; w += kK3Threads) {
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
             }
         }
         uint32_t chunk_ff;
-        const uint32_t excl = block_scan<kK3Waves>(cff, S.wsum, lane, wv, chunk_ff);
+        const uint32_t excl = block_scan<kK3Waves, uint32_t, uint32_t, false, false>(cff, S.wsum, lane, wv, chunk_ff);  // (the previous round's barriers lead)
         const uint32_t cend = min(c + (uint32_t)kChunk, n_own);
         const uint32_t align = (uint32_t)(d & 3);
         if (j0 < jhi) {

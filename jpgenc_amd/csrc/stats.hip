@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             }
         }
         uint32_t T;
-        const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true>(cnt, lds.wsum, lane, wv, T);
+        const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true, false>(cnt, lds.wsum, lane, wv, T);  // (A's barrier leads)
         if (bact) {
             lds.nzbase[b] = ex >> 16;
             lds.binfo[b] = make_uint2((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7),
