@@ -500,17 +500,8 @@ __global__ __launch_bounds__(kScanThreads) void entropy_scan_kernel(EntropyArgs 
     }
 }
 
-// The round's stuffed output is staged in LDS with one pad word after every 8 (byte
-// o at ob_at(o)): lanes write their windows 32 bytes apart, which unpadded put a
-// 32-lane store group on 4 of the 32 write banks (8-way conflicts); skewed by a word
-// per window, the group's lanes land on distinct banks.
-#ifndef K3_OB_SKEW
-#define K3_OB_SKEW 1
-#endif
-__device__ __forceinline__ uint32_t ob_at(uint32_t o) { return K3_OB_SKEW ? o + 4u * (o >> 5) : o; }
-
 struct PackLds {
-    uint8_t ob[(2 * kChunk + 8) * 9 / 8 + 8];  // stuffed output of one round (skewed, ob_at)
+    uint8_t ob[2 * kChunk + 8];  // stuffed output of one round
     uint32_t wsum[2 * kK3Waves];  // (room for 64-bit scans)
     uint64_t P, Q;
     uint32_t Lb, ftotal, split, fill, seg;
@@ -624,8 +615,8 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
             for (int q = 0; q < kWin; ++q) {
                 if (j0 + q < jhi) {
                     const uint8_t v = (uint8_t)(y[q >> 2] >> (24 - 8 * (q & 3)));
-                    S.ob[ob_at(o++)] = v;
-                    if (v == 0xFF) S.ob[ob_at(o++)] = 0;
+                    S.ob[o++] = v;
+                    if (v == 0xFF) S.ob[o++] = 0;
                 }
             }
         }
@@ -636,9 +627,9 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
         for (uint32_t w = tid; w < nw; w += kK3Threads) {
             const uint32_t s = 4 * w, e = s + 4;
             if (s >= align && e <= align + clen) {
-                __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(S.ob + ob_at(s)), reinterpret_cast<uint32_t*>(gout + s));
+                __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(S.ob + s), reinterpret_cast<uint32_t*>(gout + s));
             } else {
-                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = S.ob[ob_at(q)];
+                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = S.ob[q];
             }
         }
         d += clen;
