@@ -444,7 +444,7 @@ void Encoder::dump_stamps(const Slot& s) {
     if (!stamps_file_ || !d_dbg_) return;
     std::vector<uint64_t> h(dbg_words_);
     if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(layout(s.g)), layout(s.g).grid(),
+    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(layout(s.g), stats_wgs()), layout(s.g).grid(),
                              layout(s.g).grid()};
     FILE* f = std::fopen(stamps_file_, "wb");
     if (!f) return;
@@ -551,7 +551,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs());
     st.recs = s.d_recs;
     st.tcount = s.d_tcount;
-    st.wgs = stats_wgs_;
+    st.wgs = stats_wgs();
     st.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
     return st;
 }

@@ -156,6 +156,10 @@ class Encoder {
     // entropy workgroups: the override, else 512 for a single lane (its frames' latency:
     // -5 us at 4K) and seg_layout's default (384) beside other lanes (+3% throughput)
     uint32_t entropy_wgs() const { return entropy_wgs_ ? entropy_wgs_ : (lanes_.size() == 1 ? 512u : 0u); }
+    // statistics workgroups: 3 per CU alone (the shortest runs), 2 per CU beside other
+    // lanes (longer runs, fewer resident workgroups: measured +0.8% in the pipeline
+    // over 3 per CU; 1.5 per CU equal, 2.5 or 1 per CU slower)
+    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 0u : 512u); }
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
     // the entropy partition a slot's current frame runs on (fused K1 frames: K1's tiles)
     SegLayout slot_layout(const Slot& s) const;

@@ -194,7 +194,7 @@ struct StatsArgs {
     SegLayout seg;       // the entropy partition: the tiles the records are written in
     uint32_t* recs;      // [tiles][kTileRecords] symbol records
     uint32_t* tcount;    // [tiles] records per tile
-    uint32_t wgs = 0;    // workgroup count override (0 = automatic; diagnostics)
+    uint32_t wgs = 0;    // workgroup count (0 = 3 per CU; the pipeline passes its own, stats_grid)
     uint64_t* dbg;
 };
 
@@ -286,7 +286,8 @@ inline uint32_t entropy_tiles(const Geometry& g) {
 constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntropyTile * kStageBytesPerBlock + 128;
 
 uint32_t fdct_grid(const Geometry& g, bool solo);
-uint32_t stats_grid(const SegLayout& L);
+// statistics workgroups: wgs (0: 3 per CU), within the tile-table bound and the tile count
+uint32_t stats_grid(const SegLayout& L, uint32_t wgs = 0);
 // entropy partition of a frame: restart_mcus = 0 -> one segment over 128-block tiles
 // (2..kEntropyMaxTilesPerWg per workgroup, about 384 workgroups or wgs_override)
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override);

@@ -449,10 +449,12 @@ hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* h
     return hipGetLastError();
 }
 
-uint32_t stats_grid(const SegLayout& L) {
+uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     const uint32_t tiles = seg_tiles(L);
-    // kK2PerCu per CU, persistent over contiguous runs of at most kK2MaxRun tiles
-    const uint32_t g = tiles < 256u * kK2PerCu ? tiles : 256u * kK2PerCu;
+    // persistent over contiguous runs of at most kK2MaxRun tiles: kK2PerCu per CU by
+    // default, or wgs (kept within the tile-table bound and the tile count)
+    const uint32_t want = wgs ? wgs : 256u * kK2PerCu;
+    const uint32_t g = tiles < want ? tiles : want;
     const uint32_t need = (tiles + kK2MaxRun - 1) / kK2MaxRun;
     return g > need ? g : need;
 }
@@ -464,12 +466,7 @@ hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
-    uint32_t g = stats_grid(a.seg);
-    if (a.wgs) {  // (diagnostic override, kept within the tile-table bound)
-        const uint32_t need = (seg_tiles(a.seg) + kK2MaxRun - 1) / kK2MaxRun;
-        g = a.wgs < need ? need : (a.wgs > seg_tiles(a.seg) ? seg_tiles(a.seg) : a.wgs);
-    }
-    hipLaunchKernelGGL(stats_kernel, dim3(g), dim3(kK2Threads), 0, s, a);
+    hipLaunchKernelGGL(stats_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kK2Threads), 0, s, a);
     return hipGetLastError();
 }
 
