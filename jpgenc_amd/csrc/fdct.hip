@@ -70,7 +70,10 @@ constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's
 #ifndef K1_WAVES_SOLO
 #define K1_WAVES_SOLO 16
 #endif
-constexpr int kK1WavesSolo = K1_WAVES_SOLO, kK1WavesShared = 4;
+#ifndef K1_WAVES_SHARED
+#define K1_WAVES_SHARED 4  // (pipeline: 8 waves x 256 -1.4%, 8 x 512 -3.3%, 2 x 1024 -2.3%)
+#endif
+constexpr int kK1WavesSolo = K1_WAVES_SOLO, kK1WavesShared = K1_WAVES_SHARED;
 constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
 constexpr int kTmpBlock = 72;    // doubles per transpose block (rows of 9 doubles)
 constexpr int kTmpRow = 9;
