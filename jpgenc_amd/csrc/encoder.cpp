@@ -382,7 +382,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
     e->nap_ = env_int("JPGE_NAP", 0, 0, 1) != 0;
     e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
-    e->ext_place_ = env_int("JPGE_EXT_PLACE", 0, 0, 1) != 0;
+    e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -570,7 +570,7 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.rec = s.d_ctl + L.rec;
     e.place = reinterpret_cast<WgPlace*>(s.d_ctl + L.place);
     e.summary = reinterpret_cast<StripeSummary*>(s.d_ctl + L.summary);
-    if (ext_place_) e.flags |= kExtPlace;
+    if (ext_place_ > 0 || (ext_place_ < 0 && lanes_.size() > 1)) e.flags |= kExtPlace;
     e.host_result = s.d_result_host;
     e.seq = s.seq;
     e.ubuf = s.d_ubuf;

@@ -167,7 +167,11 @@ class Encoder {
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables
-    bool ext_place_ = false;    // JPGE_EXT_PLACE: entropy placement by the scan kernel at every size (tests)
+    // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
+    // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
+    // lanes (one small launch instead of every pack workgroup scanning all records:
+    // +0.8% in the pipeline), inline alone (one launch less per frame)
+    int ext_place_ = -1;
     int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
     bool nap_ = false;          // JPGE_NAP: lane threads sleep ~10 us between polls instead of spinning
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
