@@ -32,6 +32,9 @@ using namespace dev;
 #ifndef K3_WPE
 #define K3_WPE 8  // waves per SIMD: 64 VGPRs (measured: +4% in the pipeline over 4)
 #endif
+#ifndef K3_EMIT_MERGE
+#define K3_EMIT_MERGE 1  // a thread's 4 records written as one bit string (code kernel)
+#endif
 #ifndef K3_PACK_BRANCHY
 #define K3_PACK_BRANCHY 1  // (measured: the branch-free 64-bit form ran 6 us slower per 4K frame)
 #endif
@@ -187,6 +190,28 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         JPGE_ACC(4, tq);
         // each record into the one or two stage words it spans
         uint32_t bp = pos + ex;
+#if K3_EMIT_MERGE
+        // The thread's records are adjacent in the stream: concatenated in a 64-bit word
+        // they touch at most three stage words, of which only the first and the last
+        // can be shared with a neighbour (LDS OR); a middle word is the thread's alone
+        // (plain store).  One to three LDS writes instead of one or two atomics per
+        // record.  More than 64 bits (rare: four long codes) take the per-record path.
+        if (tl && tl <= 64) {
+            uint64_t acc = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc = (acc << cl[q]) | (cl[q] ? (uint64_t)cb[q] : 0ull);
+            const uint64_t A = acc << (64 - tl);  // MSB-aligned
+            const uint32_t sh = bp & 31, w = bp >> 5, end = sh + tl;
+            const uint32_t hi = (uint32_t)(A >> 32), lo = (uint32_t)A;
+            atomicOr(&L.stage[w], hi >> sh);
+            if (end > 32) {
+                const uint32_t v1 = sh ? (hi << (32 - sh)) | (lo >> sh) : lo;
+                if (end >= 64) L.stage[w + 1] = v1;
+                else atomicOr(&L.stage[w + 1], v1);
+                if (end > 64) atomicOr(&L.stage[w + 2], lo << (32 - sh));
+            }
+        } else
+#endif
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
 #if K3_PACK_BRANCHY
