@@ -29,8 +29,13 @@ namespace jpge {
 namespace {
 using namespace dev;
 
+#ifndef K3_GROUPS
+#define K3_GROUPS 2  // code kernel: 4-record groups per thread and round (one scan and barrier per round)
+#endif
 #ifndef K3_WPE
-#define K3_WPE 8  // waves per SIMD: 64 VGPRs (measured: +4% in the pipeline over 4)
+// waves per SIMD: one group fits 64 VGPRs at 8 (+4% in the pipeline over 4); two groups
+// need 72 (7 waves): +0.7% over one group at 8 (2 pairs on one box; 6 waves: +0.3%)
+#define K3_WPE (K3_GROUPS > 1 ? 7 : 8)
 #endif
 #ifndef K3_EMIT_MERGE
 #define K3_EMIT_MERGE 1  // a thread's 4 records written as one bit string (code kernel)
@@ -136,7 +141,8 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     const uint32_t slot = a.slot_words ? a.slot_words : (uint32_t)kTileRecords;  // record words per tile
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * slot), 0, ntl * slot * 4, 0x00020000);
-    constexpr uint32_t kRound = 4 * kK3Threads;  // records per round
+    constexpr int kGroups = K3_GROUPS;            // groups of 4 records per thread and round
+    constexpr uint32_t kRound = 4 * kGroups * kK3Threads;  // records per round
     // The workgroup's records are one stream over its tiles: tile t's count padded to a
     // multiple of 4 (so a thread's 4 records are in one tile; the padding is never
     // valid), rounds of kRound records run across tile boundaries, and the stage is
@@ -146,8 +152,8 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     for (int t = 0; t < ntl; ++t) total += (L.tcnt[t] + 3u) & ~3u;
     total = __builtin_amdgcn_readfirstlane(total);
     uint32_t cs = 0, cpre = 0;  // this thread's tile cursor (tile, its first padded index)
-    uint32_t nvalid = 0;        // valid records among the 4 prefetched
-    auto rec_load = [&](uint32_t i) -> uint4 {  // the thread's 4 records from stream index i
+    // the thread's 4 records from stream index i (nvalid: how many are records)
+    auto rec_load = [&](uint32_t i, uint32_t& nvalid) -> uint4 {
         while (cs < (uint32_t)ntl) {
             const uint32_t n = (L.tcnt[cs] + 3u) & ~3u;
             if (i < cpre + n) break;
@@ -164,22 +170,31 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rec_rs, off, 0, 0));
     };
     constexpr uint32_t kStageBits = (kStageWords - 2) * 32;
-    constexpr uint32_t kRoundMaxBits = kRound * 32;  // (a record codes at most 16 + 11 bits)
+    constexpr uint32_t kRoundMaxBits = kRound * 27;  // (a record codes at most 16 + 11 bits)
     static_assert(kStageBits > kRoundMaxBits, "the stage holds a round");
-    uint4 nxt = rec_load(4 * tid);
+    uint4 nxt[kGroups];
+    uint32_t nvn[kGroups];
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) nxt[g] = rec_load(4 * (kGroups * tid + g), nvn[g]);
     uint32_t lead = 0, pos = 0;  // bit position in the stage (lead: the carried partial word's bits)
     uint32_t par = 0;            // scan buffer of this round
     for (uint32_t r0 = 0; r0 < total; r0 += kRound) {
-        const uint4 rv = nxt;
-        const uint32_t nv = nvalid;
-        nxt = rec_load(r0 + kRound + 4 * tid);  // the next round's (prefetch)
-        const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
-        uint32_t cb[4], cl[4], tl = 0;
+        uint32_t cb[kGroups][4], cl[kGroups][4], gl[kGroups], tl = 0;
+
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t n = rec_bits(rr[q], L.tab, cb[q]);
-            cl[q] = (uint32_t)q < nv ? n : 0u;
-            tl += cl[q];
+        for (int g = 0; g < kGroups; ++g) {
+            const uint4 rv = nxt[g];
+            const uint32_t nv = nvn[g];
+            nxt[g] = rec_load(r0 + kRound + 4 * (kGroups * tid + g), nvn[g]);  // the next round's (prefetch)
+            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+            gl[g] = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t n = rec_bits(rr[q], L.tab, cb[g][q]);
+                cl[g][q] = (uint32_t)q < nv ? n : 0u;
+                gl[g] += cl[g][q];
+            }
+            tl += gl[g];
         }
         JPGE_ACC(3, tq);
         uint32_t T;
@@ -188,20 +203,22 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         const uint32_t ex = block_scan<kK3Waves, uint32_t, uint32_t, true, false>(tl, L.wsum[par], lane, wv, T);
         par ^= 1u;
         JPGE_ACC(4, tq);
-        // each record into the one or two stage words it spans
         uint32_t bp = pos + ex;
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
 #if K3_EMIT_MERGE
-        // The thread's records are adjacent in the stream: concatenated in a 64-bit word
+        // A group's 4 records are adjacent in the stream: concatenated in a 64-bit word
         // they touch at most three stage words, of which only the first and the last
         // can be shared with a neighbour (LDS OR); a middle word is the thread's alone
         // (plain store).  One to three LDS writes instead of one or two atomics per
         // record.  More than 64 bits (rare: four long codes) take the per-record path.
-        if (tl && tl <= 64) {
+        const uint32_t tg = gl[g];
+        if (tg && tg <= 64) {
             uint64_t acc = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc = (acc << cl[q]) | (cl[q] ? (uint64_t)cb[q] : 0ull);
-            const uint64_t A = acc << (64 - tl);  // MSB-aligned
-            const uint32_t sh = bp & 31, w = bp >> 5, end = sh + tl;
+            for (int q = 0; q < 4; ++q) acc = (acc << cl[g][q]) | (cl[g][q] ? (uint64_t)cb[g][q] : 0ull);
+            const uint64_t A = acc << (64 - tg);  // MSB-aligned
+            const uint32_t sh = bp & 31, w = bp >> 5, end = sh + tg;
             const uint32_t hi = (uint32_t)(A >> 32), lo = (uint32_t)A;
             atomicOr(&L.stage[w], hi >> sh);
             if (end > 32) {
@@ -210,25 +227,30 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
                 else atomicOr(&L.stage[w + 1], v1);
                 if (end > 64) atomicOr(&L.stage[w + 2], lo << (32 - sh));
             }
+            bp += tg;
         } else
 #endif
+        {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            // each record into the one or two stage words it spans
 #if K3_PACK_BRANCHY
-            if (cl[q]) {
-                const uint32_t sh = bp & 31, n = cl[q];
-                const uint32_t v = cb[q] << (32 - n);  // MSB-aligned (n >= 1)
+            if (cl[g][q]) {
+                const uint32_t sh = bp & 31, n = cl[g][q];
+                const uint32_t v = cb[g][q] << (32 - n);  // MSB-aligned (n >= 1)
                 atomicOr(&L.stage[bp >> 5], v >> sh);
                 if (sh + n > 32) atomicOr(&L.stage[(bp >> 5) + 1], v << (32 - sh));
                 bp += n;
             }
 #else
-            const uint32_t n = cl[q], sh = bp & 31;
-            const uint64_t v = n ? ((uint64_t)cb[q] << (64 - n)) >> sh : 0ull;  // MSB-aligned at bp
+            const uint32_t n = cl[g][q], sh = bp & 31;
+            const uint64_t v = n ? ((uint64_t)cb[g][q] << (64 - n)) >> sh : 0ull;  // MSB-aligned at bp
             atomicOr(&L.stage[bp >> 5], (uint32_t)(v >> 32));
             if ((uint32_t)v) atomicOr(&L.stage[(bp >> 5) + 1], (uint32_t)v);
             bp += n;
 #endif
+        }
+        }
         }
         pos += T;
         JPGE_ACC(6, tq);
