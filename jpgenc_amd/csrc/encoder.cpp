@@ -222,7 +222,7 @@ class Encoder::TablePool {
 
 struct Encoder::Slot {
     hipStream_t stream = nullptr;  // the encoder's stream (shared by all slots, not owned)
-    // 0-2, 4-5 kernel timing brackets, 7 output copied to the host (3, 6 unused)
+    // 0-2, 4-5 kernel timing brackets (3, 6, 7 unused)
     hipEvent_t ev[8] = {};
     Geometry g;
     // device workspace (capacities)
@@ -772,9 +772,11 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
     f.len = len;
     if (flags & kFlagDeviceOutput) return kOk;
     if (len > f.cap) return kErrNoSpace;
+    // Queued on the lane's stream and not awaited here: every caller synchronises the
+    // stream afterwards (a batch at its end), and the slot's next pack kernel is behind
+    // the copy in stream order.  (Waiting here held the lane's host thread for the
+    // stream's queued kernels too: 77 GPix/s with host outputs.)
     JPGE_HIP(hipMemcpyAsync(f.out, s.out_dev, len, hipMemcpyDeviceToHost, s.stream));
-    JPGE_HIP(hipEventRecord(s.ev[7], s.stream));
-    JPGE_HIP(wait_event(s.ev[7]));
     return kOk;
 }
 
