@@ -547,6 +547,30 @@ __global__ __launch_bounds__(kScanThreads) void entropy_scan_kernel(EntropyArgs 
     }
 }
 
+// entropy_place_kernel — the scan kernel's place mode in a smaller workgroup for
+// grids up to kPlaceSmallMaxWgs (restart off): a 4-wave workgroup finds a CU beside
+// the other lanes' kernels sooner than a 16-wave one, and the lane's stream waits on it.
+#ifndef K3_PLACE_THREADS
+#define K3_PLACE_THREADS 256
+#endif
+constexpr int kPlaceThreads = K3_PLACE_THREADS;
+constexpr uint32_t kPlaceSmallMaxWgs = 4096;
+__global__ __launch_bounds__(kPlaceThreads) void entropy_place_kernel(EntropyArgs a, uint32_t G) {
+    __shared__ uint32_t wsum[2 * (kPlaceThreads / 64)];
+    const RecView R{a.rec, G};
+    scan_records<kPlaceThreads / 64>(a, R, wsum, threadIdx.x, [&](uint32_t k, uint64_t p, uint64_t q, uint32_t o) {
+        a.place[k] = make_place(R, k, p, q, o, a);
+    });
+}
+// the place mode's launch: the small kernel where it applies, else the scan kernel
+hipError_t launch_place(const EntropyArgs& b, uint32_t G, hipStream_t s) {
+    if (!b.rst.mcus && G <= kPlaceSmallMaxWgs && kPlaceThreads < kScanThreads)
+        hipLaunchKernelGGL(entropy_place_kernel, dim3(1), dim3(kPlaceThreads), 0, s, b, G);
+    else
+        hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
+    return hipGetLastError();
+}
+
 struct PackLds {
     uint8_t ob[2 * kChunk + 8];  // stuffed output of one round
     uint32_t wsum[2 * kK3Waves];  // (room for 64-bit scans)
@@ -767,8 +791,7 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
     if (G > kInlineScanMaxWgs || (a.flags & kExtPlace) || a.rst.mcus) {
         if (!a.place) return hipErrorInvalidValue;
         b.flags |= kExtPlace;
-        hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = launch_place(b, G, s)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
     return hipGetLastError();
@@ -792,8 +815,7 @@ hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s) {
     EntropyArgs b = a;
     b.flags |= kExtPlace;
     if (!a.rst.mcus) {  // (restart intervals: placed by launch_entropy_code_summary)
-        hipLaunchKernelGGL(entropy_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, b, G, 0);
-        const hipError_t e = hipGetLastError();
+        const hipError_t e = launch_place(b, G, s);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
