@@ -132,13 +132,14 @@ constexpr size_t kHdrMax = 4096;           // headers SOI .. SOS (<= 20 + 2*69 +
 
 // Control block, zeroed at the start of every frame by the first kernel (K1).
 struct CtlLayout {
-    size_t cnt, key, rec, total;  // [0, total): zeroed by K1 every frame
+    size_t cnt, key, rec, done, total;  // [0, total): zeroed by K1 every frame
     size_t place, summary, alloc;  // not zeroed (written before they are read)
     explicit CtlLayout(uint32_t ntiles) {  // ntiles: entropy workgroups (records)
         size_t o = 0;
         cnt = o; o += align_up((size_t)kHistReplicas * 4 * 256 * 4, 256);
         key = o; o += align_up(4 * 256 * 8, 256);
         rec = o; o += align_up((size_t)ntiles * kEntropyRecordBytes, 256);
+        done = o; o += 256;
         total = o;
         place = o; o += align_up((size_t)ntiles * sizeof(WgPlace), 256);
         summary = o; o += 256;
@@ -383,6 +384,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->nap_ = env_int("JPGE_NAP", 0, 0, 1) != 0;
     e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
     e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
+    e->place_in_code_ = env_int("JPGE_PLACE_IN_CODE", 1, 0, 1) != 0;
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -570,7 +572,13 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.rec = s.d_ctl + L.rec;
     e.place = reinterpret_cast<WgPlace*>(s.d_ctl + L.place);
     e.summary = reinterpret_cast<StripeSummary*>(s.d_ctl + L.summary);
-    if (ext_place_ > 0 || (ext_place_ < 0 && lanes_.size() > 1)) e.flags |= kExtPlace;
+    if (ext_place_ > 0 || (ext_place_ < 0 && lanes_.size() > 1)) {
+        e.flags |= kExtPlace;
+        // the last code workgroup places every workgroup (no placement launch); the
+        // counter is in the block K1 zeroes (the fused K1 does not zero it)
+        if (place_in_code_ && !s.fused && !s.rst.mcus && slot_layout(s).grid() <= kPlaceInCodeMaxWgs)
+            e.done = reinterpret_cast<uint32_t*>(s.d_ctl + L.done);
+    }
     e.host_result = s.d_result_host;
     e.seq = s.seq;
     e.ubuf = s.d_ubuf;
@@ -1100,6 +1108,7 @@ int Encoder::stripe_code(const uint32_t counts[1024], const uint64_t first[1024]
     if (const int st = build_tables_from(s, counts, first, true)) return st;
     if (const int st = import_tables_copy(s)) return st;
     EntropyArgs e = entropy_args(s);
+    e.done = nullptr;  // (stripes: placed by the stripe phases)
     JPGE_HIP(launch_entropy_code_summary(e, s.stream));
     JPGE_HIP(hipMemcpyAsync(sum, e.summary, sizeof(StripeSummary), hipMemcpyDeviceToHost, s.stream));
     JPGE_HIP(hipStreamSynchronize(s.stream));
@@ -1171,6 +1180,7 @@ int Encoder::stripe_pack(const StripeSummary* all, int n, int index, uint8_t* ou
     s.seq = ++seq_counter_;
     s.h_result[2] = 0;
     EntropyArgs e = entropy_args(s);
+    e.done = nullptr;  // (stripes: placed by the stripe phases)
     if (s.rst.mcus) {
         e.out_base = q_ext;  // (placed in phase 3, relative to the stripe's start)
     } else {

@@ -172,6 +172,7 @@ class Encoder {
     // lanes (one small launch instead of every pack workgroup scanning all records:
     // +0.8% in the pipeline), inline alone (one launch less per frame)
     int ext_place_ = -1;
+    bool place_in_code_ = true;  // JPGE_PLACE_IN_CODE: the last code workgroup places (pipeline)
     int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
     bool nap_ = false;          // JPGE_NAP: lane threads sleep ~10 us between polls instead of spinning
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps

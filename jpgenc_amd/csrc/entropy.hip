@@ -68,7 +68,7 @@ struct K3Lds {
     uint32_t stage[kStageWords];  // the tile's big-endian bit stream
     uint32_t tab[4 * 256];        // (len << 16) | code
     uint32_t tcnt[kTcntSlots];    // symbol records of each of the workgroup's tiles
-    uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds)
+    alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
     uint32_t cnt8[8];
     uint32_t carry;
 };
@@ -94,6 +94,9 @@ __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, ui
     bits = ((ent & 0xFFFF) << nb) | (r & 0xFFFF);
     return (ent >> 16) + nb;
 }
+
+// every workgroup's WgPlace from the records (the placement scan), kK3Threads threads
+__device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int tid);
 
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_WPE))) void entropy_code_kernel(
     EntropyArgs a) {
@@ -317,6 +320,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     __syncthreads();
     if (tid < 3) {
         uint32_t* rec = reinterpret_cast<uint32_t*>(a.rec + (uint64_t)wg * kEntropyRecordBytes);
+        uint4 v;
         if (tid == 0) {
             // first 8 bits; last 8 bits (the 16-bit window holding them is inside R).
             // A stream shorter than a byte (a 4:4:4 restart interval of one MCU) is
@@ -329,11 +333,34 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
             } else {
                 tail = (uint32_t)R8[0] >> (8 - Lb);
             }
-            *reinterpret_cast<uint4*>(rec + 8) = make_uint4(Lb, head | (tail << 8), 0u, 0u);
+            v = make_uint4(Lb, head | (tail << 8), 0u, 0u);
         } else {
             const int b0 = 4 * (tid - 1);  // ff[0..3], ff[4..7]
-            *reinterpret_cast<uint4*>(rec + b0) =
-                make_uint4(L.cnt8[b0], L.cnt8[b0 + 1], L.cnt8[b0 + 2], L.cnt8[b0 + 3]);
+            v = make_uint4(L.cnt8[b0], L.cnt8[b0 + 1], L.cnt8[b0 + 2], L.cnt8[b0 + 3]);
+        }
+        uint32_t* dst = rec + (tid == 0 ? 8 : 4 * (tid - 1));
+        if (a.done) {
+            // device-coherent stores (through this XCD's L2), complete before the count
+            // below; a release fence would write back the whole L2 (26% slower)
+            __hip_atomic_store(dst + 0, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            vm_drain();
+        } else {
+            *reinterpret_cast<uint4*>(dst) = v;
+        }
+    }
+    if (a.done) {
+        // Placement by the last workgroup to finish (no placement launch between this
+        // kernel and the pack kernel): every workgroup counts itself after its record is
+        // visible device-wide; the one that completes the count reads all records.
+        __syncthreads();
+        if (tid == 0) L.carry = atomicAdd(a.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+        __syncthreads();
+        if (L.carry) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the other workgroups' records)
+            place_all(a, gridDim.x, &L.wsum[0][0], tid);
         }
     }
     JPGE_STAMP(2);
@@ -545,6 +572,13 @@ __global__ __launch_bounds__(kScanThreads) void entropy_scan_kernel(EntropyArgs 
         sm.tail = (R(G - 1)[kRecEdge] >> 8) & 0xFF;
         *a.summary = sm;
     }
+}
+
+__device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int tid) {
+    const RecView R{a.rec, G};
+    scan_records<kK3Waves>(a, R, wsum, tid, [&](uint32_t k, uint64_t p, uint64_t q, uint32_t o) {
+        a.place[k] = make_place(R, k, p, q, o, a);
+    });
 }
 
 // entropy_place_kernel — the scan kernel's place mode in a smaller workgroup for
@@ -788,7 +822,10 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
-    if (G > kInlineScanMaxWgs || (a.flags & kExtPlace) || a.rst.mcus) {
+    if (a.done) {  // placed by the code kernel's last workgroup
+        if (!a.place || a.rst.mcus || G > kPlaceInCodeMaxWgs) return hipErrorInvalidValue;
+        b.flags |= kExtPlace;
+    } else if (G > kInlineScanMaxWgs || (a.flags & kExtPlace) || a.rst.mcus) {
         if (!a.place) return hipErrorInvalidValue;
         b.flags |= kExtPlace;
         if ((e = launch_place(b, G, s)) != hipSuccess) return e;

@@ -235,6 +235,7 @@ struct EntropyArgs {
     uint64_t out_cap;
     uint8_t* ubuf;           // per-workgroup unstuffed regions (entropy_ubuf_bytes)
     uint8_t* rec;            // [entropy_grid][kEntropyRecordBytes] code -> pack kernel records
+    uint32_t* done = nullptr;  // (zeroed per frame) code workgroups finished: the last one places all
     uint64_t* host_result;   // mapped pinned host memory: [0] .jpg bytes, [1] no-space (4),
                              // [2] reserved (0), [3] = seq, written last
     uint64_t seq;            // the frame's sequence number
@@ -312,5 +313,6 @@ hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s);
 // grids above this many workgroups place by a separate scan (each pack workgroup
 // scanning every record would read G^2 records)
 constexpr uint32_t kInlineScanMaxWgs = 1024;
+constexpr uint32_t kPlaceInCodeMaxWgs = 4096;  // grids the last code workgroup places
 
 }  // namespace jpge
