@@ -144,13 +144,15 @@ def test_entropy_workgroup_partitions_4k(wgs):
         enc.close()
 
 
-# Placement by the separate scan kernel (large grids: 16K) must agree with the
-# pack kernel's own scan at every partition.
+# Placement computed once for all workgroups — by the code kernel's last workgroup
+# (in_code=1, the pipeline's default) or by the placement kernel (in_code=0) — must
+# agree with the pack kernel's own scan at every partition.
+@pytest.mark.parametrize("in_code", [0, 1])
 @pytest.mark.parametrize("wgs", [1, 5, 100000])
 @pytest.mark.parametrize("w,h,kind,quality", [(500, 300, 1, 100), (1040, 16, 0, 75), (16, 1040, 0, 50),
                                               (1920, 1080, 0, 90)])
-def test_entropy_scan_kernel_placement(wgs, w, h, kind, quality):
-    enc = _encoder_with_env(JPGE_ENTROPY_WGS=wgs, JPGE_EXT_PLACE=1)
+def test_entropy_scan_kernel_placement(in_code, wgs, w, h, kind, quality):
+    enc = _encoder_with_env(JPGE_ENTROPY_WGS=wgs, JPGE_EXT_PLACE=1, JPGE_PLACE_IN_CODE=in_code)
     try:
         rgb = J.synth_rgb8(57 + kind + w, w, h, kind=kind)
         assert enc.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
