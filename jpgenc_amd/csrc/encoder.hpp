@@ -174,7 +174,7 @@ class Encoder {
     int ext_place_ = -1;
     bool place_in_code_ = true;  // JPGE_PLACE_IN_CODE: the last code workgroup places (pipeline)
     int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
-    bool nap_ = false;          // JPGE_NAP: lane threads sleep ~10 us between polls instead of spinning
+    bool nap_ = false;          // lane threads sleep ~10 us between polls instead of spinning (default: >1 lane; JPGE_NAP)
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
     uint64_t* d_dbg_ = nullptr;
