@@ -558,6 +558,13 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.recs = s.d_recs;
     st.tcount = s.d_tcount;
     st.wgs = stats_wgs();
+    if (!stats_wgs_ && lanes_.size() > 1) {
+        // frames under ~3 MPix (fewer than 3 tiles per workgroup at 384): about 3 tiles per
+        // workgroup, not one each (a workgroup's fixed costs, its first load not overlapped:
+        // 1080p batch +9%); 4K and larger keep the 2-per-CU grid
+        const uint32_t t = seg_tiles(st.seg);
+        if (t < 3u * 384u) st.wgs = std::max(1u, (t + 2) / 3);
+    }
     st.dbg = d_dbg_ ? d_dbg_ + 65536 * kStampSlots : nullptr;
     return st;
 }

@@ -779,7 +779,10 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
         uint32_t G = 1;
         if (nt > 1) {
             const uint32_t lo = (nt + kMaxTiles - 1) / kMaxTiles, hi = nt;
-            G = want < lo ? lo : (want > hi ? hi : want);
+            // (the pipeline's default on frames under 768 tiles: 2 tiles per workgroup, not
+            // one each: 1080p batch +8%)
+            const uint32_t w = wgs_override ? want : (nt < 2u * want ? (nt + 1) / 2 : want);
+            G = w < lo ? lo : (w > hi ? hi : w);
         }
         L.nseg = 1;
         L.sblk = L.lblk = nb;
