@@ -45,6 +45,9 @@ constexpr int kCopyWords = 2 * 256 + 4;
 constexpr int kDcCopyWords = 2 * 16 + 4;
 
 constexpr int kMaxNz = kK2Blocks * 63;  // AC non-zeros of a tile, at most
+#ifndef K2_DROT
+#define K2_DROT 128
+#endif
 #ifndef K2_PERCU
 #define K2_PERCU 3
 #endif
@@ -263,7 +266,9 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
         JPGE_ACC(2, tq);
         // ---- D: symbols ----
         const uint32_t N = lds.tot;
-        for (uint32_t e = tid; e < N; e += kK2Threads) {
+        // (rotated by K2_DROT: the loop's partial last round falls first on the waves past
+        // the block lanes, which code the DC and EOB records after it)
+        for (uint32_t e = (tid + K2_DROT) & (kK2Threads - 1); e < N; e += kK2Threads) {
             const uint32_t ent = lds.nz[e];
             const int v = (int16_t)(ent & 0xFFFF);
             const int p = (int)((ent >> 16) & 63), blk = (int)(ent >> 22);
