@@ -10,7 +10,7 @@ Only rank 0 prints.
 Workloads (a step = one pass of the full encode path over a batch of synthetic
 frames resident in HBM: colour/4:2:0/FDCT/quantise + statistics kernels, host
 Huffman-table build, entropy code + pack kernels, finished .jpg bytes in HBM):
-  4k-frames  (default; BASELINE metric, SURVEY 8(e) frames): F = 768 frames of
+  4k-frames  (default; BASELINE metric, SURVEY 8(e) frames): F = 3072 frames of
              3840x2160 Q90 per GPU per step, cycling over D = 32 distinct inputs
              (800 MB > the 256 MB Infinity Cache, so K1 reads from HBM); frames are
              independent, each rank encodes its own (weak scaling, no data-path
@@ -22,10 +22,13 @@ Huffman-table build, entropy code + pack kernels, finished .jpg bytes in HBM):
   16k-striped (config 5): one 16384^2 frame per step, row-striped over the ranks.
   ppm-files  (SURVEY 8(f) rank 1): PPM files -> .jpg files (PCIe-inclusive).
 
-The 4k-frames line carries: `roofline` = the dominant kernel in situ (HIP events on
-its lane's stream inside the timed region), `roofline_dct_stage` = K1 alone (the
-BASELINE figure, with its HBM-read-only fraction), `roofline_pipeline`, per-stage
-rooflines (algorithmic bytes per launch), `verified` (every output of
+The 4k-frames line carries: `roofline` = the dominant kernel alone on the GPU (its
+exclusive time: a 1-lane encoder after the timed region, HIP events bound to the
+kernel's own dispatch; checked against the step: launches x duration <= ms_per_step),
+`roofline_dct_stage` = K1 alone (the BASELINE figure, with its HBM-read-only
+fraction), `roofline_pipeline`, per-kernel rooflines in situ (`stages`, overlapping
+lanes: diagnostic) and alone (`stages_solo`; algorithmic bytes per launch, DESIGN.md
+§4), `devices` (ranks, distinct GPUs, ranks per GPU), `verified` (every output of
 the last timed step byte-compared with the host-path encode of its frame, and a
 sample with the CPU oracle), `d2h` (device RGB -> .jpg bytes in pinned host
 memory, SURVEY 8(d)'s end-to-end definition) and `cpu_baseline` (the test-only
@@ -66,7 +69,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=None,
-                    help="frames per GPU per step (4k-frames: 768; batch1080: the whole batch, 256)")
+                    help="frames per GPU per step (4k-frames: 3072, so the default 20 steps span ~3 s; "
+                         "batch1080: the whole batch, 256)")
     ap.add_argument("--distinct", type=int, default=32, help="4k-frames: distinct input frames the step cycles over")
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--width", type=int, default=W4K)
@@ -91,6 +95,9 @@ def parse(argv=None):
                     help="4k-frames: subsampling mode (jpge.h JPGE_S*: 420 = the reference's S420_m; "
                          "444, 422, 411, 4200 = S420, 4201 = S420_lm are extensions)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="rehearse N ranks on fewer than N GPUs (ranks share devices; the line says so). "
+                         "Without it, --gpus N refuses to run on a node with fewer than N GPUs")
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
     ap.add_argument("--event-every", type=int, default=4,
                     help="bracket the kernels of every N-th frame with HIP events (each event costs GPU time)")
@@ -176,12 +183,33 @@ def sum_over_ranks(pg, v: float) -> float:
     return float(t.item())
 
 
-def device_for(local: int) -> int:
-    """This rank's GPU: LOCAL_RANK, wrapped when the box has fewer GPUs than ranks (a
-    rehearsal of N ranks on one GPU; the driver's N-GPU runs have one GPU per rank)."""
+def visible_devices() -> int:
+    """GPUs this node shows (torch.cuda.device_count() does not initialise the GPU on
+    this image; JPGE_BENCH_DEVICE_COUNT overrides it for the CPU tests)."""
+    if os.environ.get("JPGE_BENCH_DEVICE_COUNT"):
+        return int(os.environ["JPGE_BENCH_DEVICE_COUNT"])
     import torch
 
-    return local % max(1, torch.cuda.device_count())
+    return torch.cuda.device_count()
+
+
+def device_plan(world: int, allow_shared: bool) -> dict:
+    """One GPU per rank, or a refusal: N ranks on fewer than N GPUs would publish a
+    scaling point that no N-GPU run produced.  --allow-shared-gpu rehearses N ranks on
+    fewer GPUs (rank r on GPU r mod count); the line then says so (`devices`)."""
+    n = visible_devices()
+    if world > n and not allow_shared:
+        raise SystemExit(f"bench: {world} rank(s) need {world} GPU(s), this node shows {n}; "
+                         f"--allow-shared-gpu rehearses ranks sharing GPUs (not a scaling point)")
+    distinct = min(world, max(n, 1))
+    return {"ranks": world, "devices_visible": n, "devices_distinct": distinct,
+            "ranks_per_device": -(-world // distinct), "shared": world > distinct}
+
+
+def device_for(local: int) -> int:
+    """This rank's GPU: LOCAL_RANK (wrapped only under --allow-shared-gpu, which
+    device_plan checked before any GPU work)."""
+    return local % max(1, visible_devices())
 
 
 def gather_group(world: int):
@@ -190,7 +218,7 @@ def gather_group(world: int):
     import torch
     import torch.distributed as dist
 
-    return dist.new_group(backend="nccl" if torch.cuda.device_count() >= world else "gloo")
+    return dist.new_group(backend="nccl" if visible_devices() >= world else "gloo")
 
 
 def frame_seed(rank: int, i: int) -> int:
@@ -324,7 +352,7 @@ def run_dist_check(args, rank, local, world, pg):
     frames = sum_over_ranks(pg, float(len(share)))
     if rank == 0:
         print(json.dumps({"metric": "dist-check", "value": n, "unit": "ranks", "n_gpus": world, "max_time": dt,
-                          "batch_frames": frames, "rank0_first": share[:3]}), flush=True)
+                          "batch_frames": frames, "rank0_first": share[:3], "devices": args.devices}), flush=True)
 
 
 def run_striped16k(args, rank, local, world, pg):
@@ -390,6 +418,7 @@ def run_striped16k(args, rank, local, world, pg):
                                          if restart else
                                          "DC seeds, histogram sum/min, summaries; segments gathered to rank 0)")),
                        "restart_mcus": restart, "jpeg_bytes": int(n)},
+            "devices": args.devices,
         }), flush=True)
     enc.close()
 
@@ -441,6 +470,7 @@ def run_ppm_files(args, rank, local, world, pg):
                            "width": W, "height": H, "quality": args.quality, "files_per_step_per_gpu": F,
                            "avg_jpeg_bytes": int(nbytes / (args.steps * F)),
                            "parallelism": f"files sharded over {world} GPU(s)"},
+                "devices": args.devices,
             }), flush=True)
         enc.close()
     finally:
@@ -557,6 +587,7 @@ def run_batch1080(args, rank, local, world, pg):
                 "method": "every frame of the last step, as gathered on rank 0, byte-compared with the host-path "
                           "encode of the same frame"},
             "host_cpu": host_cpu_use(cg0, cg1, dt),
+            "devices": args.devices,
         }
         print(json.dumps(line), flush=True)
     enc.close()
@@ -576,7 +607,7 @@ def run_frames(args, rank, local, world, pg):
     enc = J.Encoder(local, lanes=args.lanes)
     enc.set_subsampling(args.subsampling)
     W, H = args.width, args.height
-    F = args.frames or 768
+    F = args.frames or 3072
     D = max(1, min(args.distinct, F))
     pitch = W * 3
     cap = out_capacity(J, W, H)
@@ -692,34 +723,57 @@ def run_frames(args, rank, local, world, pg):
     cb = 2.0 * 64 * (yh * yv + 2) / (64 * yh * yv)  # int16 coefficient bytes per pixel (4:2:0: 3)
     # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3
     rec_bytes = 4.0 * tm["symbols"] / max(1, tm["frames"])
+    # per-kernel algorithmic bytes per launch; the entropy stage is two
+    # kernels: code (records -> the unstuffed bit stream) and pack (-> stuffed .jpg)
     alg = {
         "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
         "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 4 B each"),
-        "entropy_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + entropy-coded bytes written"),
+        "entropy_code_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + bit stream written (~.jpg size)"),
+        "entropy_pack_kernel": (2.0 * avg_jpeg, "bit stream read + stuffed .jpg bytes written"),
     }
+    stage_alg = {"entropy_stage": (rec_bytes + avg_jpeg, "symbol records read 4 B each + .jpg bytes written")}
+    tm_key = {"fdct_kernel": "fdct_sum", "stats_kernel": "dc_stats_sum", "entropy_code_kernel": "code_sum",
+              "entropy_pack_kernel": "pack_sum", "entropy_stage": "entropy_sum"}
+    pmc_key = {"entropy_stage": "entropy_kernel"}
 
     def rooflines(tm):
         nfr = max(1, tm["frames"])
-        ms = {"fdct_kernel": tm["fdct_sum"] / nfr, "stats_kernel": tm["dc_stats_sum"] / nfr,
-              "entropy_kernel": tm["entropy_sum"] / nfr}
         out = {}
-        for name, (b, what) in alg.items():
-            ach = b / (ms[name] * 1e-3) / 1e9 if ms[name] > 0 else 0.0  # (0: --no-kernel-events)
+        for name, (b, what) in list(alg.items()) + list(stage_alg.items()):
+            ms = tm[tm_key[name]] / nfr
+            ach = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # (0: --no-kernel-events)
             out[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
-                         "alg_bytes_per_launch": int(b), "alg_bytes": what, "avg_kernel_ms": round(ms[name], 5),
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(pmc_key.get(name, name)),
+                         "alg_bytes_per_launch": int(b), "alg_bytes": what, "avg_kernel_ms": round(ms, 5),
                          "timed_launches": tm["frames"]}
         # the north star's "HBM-read roofline": K1's RGB8 read alone (3 B/px)
         k1 = out["fdct_kernel"]
-        if ms["fdct_kernel"] > 0:
-            rd = 3.0 * npx / (ms["fdct_kernel"] * 1e-3) / 1e9
+        ms1 = tm["fdct_sum"] / nfr
+        if ms1 > 0:
+            rd = 3.0 * npx / (ms1 * 1e-3) / 1e9
             k1["read_achieved"] = round(rd, 1)
             k1["read_frac"] = round(rd / HBM_PEAK_GBS, 4)
         return out
 
-    stages = rooflines(tm)  # in situ: the timed region, lanes side by side
+    stages = rooflines(tm)  # in situ: the timed region, lanes side by side (overlapping: diagnostic)
     stages_solo = rooflines(tm_solo) if tm_solo else None
-    dominant = max(stages, key=lambda k: stages[k]["avg_kernel_ms"])
+    ms_step = dt_max / args.steps * 1e3
+    # The headline roofline: the dominant kernel (longest exclusive time) ALONE on the GPU
+    # (the solo pass), its duration from events bound to its own dispatch, so the figure
+    # can be recomputed from a rocprofv3 kernel trace.  In the timed region four lanes'
+    # kernels overlap, so an in-situ duration is wall time shared with the other lanes.
+    roofline = None
+    if stages_solo:
+        dominant = max(alg, key=lambda k: stages_solo[k]["avg_kernel_ms"])
+        roofline = dict(kernel=dominant, timing="solo (1-lane encoder after the timed region; HIP events bound "
+                                                "to the kernel's dispatch, hipExtLaunchKernel)", **stages_solo[dominant])
+        # exclusive time of one launch x launches per step cannot exceed the step
+        spent = F * roofline["avg_kernel_ms"]
+        roofline["check"] = {"launches_per_step": F, "launches_x_avg_ms": round(spent, 3),
+                             "ms_per_step": round(ms_step, 3), "ok": spent <= ms_step}
+        if spent > ms_step:
+            raise SystemExit(f"bench: roofline check failed: {F} launches x {roofline['avg_kernel_ms']} ms "
+                             f"= {spent:.3f} ms > {ms_step:.3f} ms per step")
     # whole pipeline: every kernel's algorithmic bytes per frame, over the wall time
     pipe_bytes = sum(b for b, _ in alg.values())
     pipe_ach = pipe_bytes * F * args.steps * world / dt_max / 1e9
@@ -749,17 +803,19 @@ def run_frames(args, rank, local, world, pg):
                 "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
                 "avg_jpeg_bytes": int(avg_jpeg),
             },
-            # dominant kernel, timed in situ (HIP events on its lane's stream, lanes side by side)
-            "roofline": dict(kernel=dominant, timing="in situ", **stages[dominant]),
+            # dominant kernel alone (exclusive time; see above)
+            "roofline": roofline,
             # BASELINE.json's "% HBM roofline on DCT stage" (6 B/px; read-only 3 B/px): the kernel alone
             "roofline_dct_stage": dict(kernel="fdct_kernel", timing="solo", **stages_solo["fdct_kernel"])
             if stages_solo else dict(kernel="fdct_kernel", timing="in situ", **stages["fdct_kernel"]),
             "roofline_pipeline": pipeline,
             "stages": stages,
             "stages_solo": stages_solo,
-            "kernel_events": f"in situ: HIP events around every {args.event_every}th frame's kernels on its lane's "
-                             f"stream; solo: every frame of {args.solo_batches} batches of {D} on a 1-lane encoder "
-                             f"after the timed region",
+            "kernel_events": f"each kernel of a sampled frame launched with its own HIP events bound to its "
+                             f"dispatch (hipExtLaunchKernel). stages: in situ, every {args.event_every}th frame in "
+                             f"the timed region (4 lanes overlap: a diagnostic, not exclusive time); stages_solo: "
+                             f"every frame of {args.solo_batches} batches of {D} on a 1-lane encoder after the "
+                             f"timed region",
             "step_ms": {"min": round(min(step_t) * 1e3, 3), "median": round(sorted(step_t)[len(step_t) // 2] * 1e3, 3),
                         "max": round(max(step_t) * 1e3, 3)},
             "lanes": enc.lanes(),
@@ -788,8 +844,10 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        device_plan(args.gpus, args.allow_shared_gpu)  # refuse before starting any rank
         sys.exit(spawn(args.gpus, argv))  # (the parent never touches a GPU)
     rank, local, world, pg = dist_setup(args.gpus)
+    args.devices = device_plan(world, args.allow_shared_gpu)
     run = {"4k-frames": run_frames, "batch1080": run_batch1080, "16k-striped": run_striped16k,
            "ppm-files": run_ppm_files, "dist-check": run_dist_check}[args.workload]
     try:

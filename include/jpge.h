@@ -54,16 +54,19 @@ typedef struct {
     int status;         /* [out] jpge_status of this frame */
 } jpge_frame;
 
-/* Per-kernel device times of the last timed frame (ms, HIP events on the encoder's
- * stream; see jpge_set_timing for sampling). */
+/* Per-kernel device times of the last timed frame (ms; see jpge_set_timing for
+ * sampling).  Each kernel of a timed frame is launched with its own pair of HIP
+ * events bound to its dispatch (hipExtLaunchKernel), so a kernel's figure is its
+ * execution time as rocprofv3 reports it, without launch gaps. */
 typedef struct {
     float fdct;     /* K1: colour + 4:2:0 + FDCT + quantise */
     float dc_stats; /* K2: DC chain + RLE/category symbol histograms + first-occurrence keys */
-    float entropy;  /* K3: Huffman emission + MCU interleave + fill + stuffing */
+    float entropy;  /* K3: code kernel start .. pack kernel end (Huffman emission, MCU interleave, fill, stuffing) */
     float total;    /* K1 start .. K3 end of that frame (includes the queued work of other frames) */
     double fdct_sum, dc_stats_sum, entropy_sum; /* accumulated since jpge_reset_timing (ms) */
     uint64_t frames;                            /* frames accumulated */
     uint64_t symbols; /* Huffman-coded symbols of those frames (= K2's 4-byte symbol records) */
+    double code_sum, pack_sum; /* K3's entropy_code_kernel and entropy_pack_kernel alone (ms, accumulated) */
 } jpge_timing;
 
 const char* jpge_strerror(int status);

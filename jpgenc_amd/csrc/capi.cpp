@@ -94,6 +94,8 @@ int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
     t->entropy_sum = k.entropy_sum;
     t->frames = k.frames;
     t->symbols = k.symbols;
+    t->code_sum = k.code_sum;
+    t->pack_sum = k.pack_sum;
     return JPGE_OK;
 }
 

@@ -1,11 +1,25 @@
 // Device helpers shared by the jpge kernels (fdct.hip, stats.hip, entropy.hip).
 // Included only by HIP translation units.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "kernels.hpp"
+
+namespace jpge {
+// Launch `kernel` on s, through hipExtLaunchKernel with the timer's events when
+// one is given (KTimer, kernels.hpp), else as a plain launch.
+template <typename F, typename... Args>
+inline hipError_t launch_timed(const KTimer* t, F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    if (t && t->start && t->stop)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, t->start, t->stop, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+    return hipGetLastError();
+}
+}  // namespace jpge
 
 #pragma clang fp contract(off)
 

@@ -412,7 +412,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
             std::unique_ptr<Slot> s(new Slot());
             s->stream = ln->stream;
             for (int k = 0; k < 8; ++k)
-                JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], (k == 3 || k >= 6) ? hipEventDisableTiming : hipEventDefault));
+                JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], hipEventDefault));
             JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
             JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
             JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
@@ -666,9 +666,9 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
     s.tables_done.store(0, std::memory_order_relaxed);
     s.export_queued.store(0, std::memory_order_relaxed);
-    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[0], s.stream));
-    JPGE_HIP(launch_fdct(a, s.stream));
-    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[1], s.stream));
+    // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
+    const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
+    JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
     if (s.fused) {
         FixupArgs fx;
         fx.tinfo = s.d_tinfo;
@@ -677,11 +677,10 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         fx.ntiles = fused_tiles(g);
         fx.tiles_per_row = (g.mw + kFusedTileMcus - 1) / kFusedTileMcus;
         fx.hist = a.hist;
-        JPGE_HIP(launch_dc_fixup(fx, s.stream));
+        JPGE_HIP(launch_dc_fixup(fx, s.stream, s.timed ? &t2 : nullptr));
     } else {
-        JPGE_HIP(launch_stats(st2, s.stream));
+        JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2 : nullptr));
     }
-    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[2], s.stream));
     s.seq = ++seq_counter_;
     s.hist = st2.hist;
     if (export_hist)
@@ -761,24 +760,28 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
     e.exp_key = exp ? exp->d_hist_host->key : nullptr;
     e.exp_seq = exp ? &exp->d_hist_host->seq : nullptr;
     e.exp_seqv = exp ? exp->seq : 0;
-    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[4], s.stream));
-    JPGE_HIP(launch_entropy(e, s.stream));
-    if (s.timed) JPGE_HIP(hipEventRecord(s.ev[5], s.stream));
+    const KTimer tc{s.ev[4], s.ev[5]}, tp{s.ev[6], s.ev[7]};
+    JPGE_HIP(launch_entropy(e, s.stream, s.timed ? &tc : nullptr, s.timed ? &tp : nullptr));
     return kOk;
 }
 
 int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
     if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_)) return w;
     if (s.timed) {
-        JPGE_HIP(wait_event(s.ev[5]));
+        JPGE_HIP(wait_event(s.ev[7]));
         std::lock_guard<std::mutex> g(times_mu_);
+        float code = 0, pack = 0;
         hipEventElapsedTime(&times_.fdct, s.ev[0], s.ev[1]);
-        hipEventElapsedTime(&times_.dc_stats, s.ev[1], s.ev[2]);
-        hipEventElapsedTime(&times_.entropy, s.ev[4], s.ev[5]);
-        hipEventElapsedTime(&times_.total, s.ev[0], s.ev[5]);
+        hipEventElapsedTime(&times_.dc_stats, s.ev[2], s.ev[3]);
+        hipEventElapsedTime(&code, s.ev[4], s.ev[5]);
+        hipEventElapsedTime(&pack, s.ev[6], s.ev[7]);
+        hipEventElapsedTime(&times_.entropy, s.ev[4], s.ev[7]);
+        hipEventElapsedTime(&times_.total, s.ev[0], s.ev[7]);
         times_.fdct_sum += times_.fdct;
         times_.dc_stats_sum += times_.dc_stats;
         times_.entropy_sum += times_.entropy;
+        times_.code_sum += code;
+        times_.pack_sum += pack;
         times_.frames += 1;
         times_.symbols += s.symbols;
     }
@@ -847,6 +850,11 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
             std::fclose(f);
         }
     }
+    int bad = st;
+    for (int i = 0; i < n && !bad; ++i) bad = fr[i].status;
+    if (bad)  // an error exit (run_lane's early returns included) may leave device-to-host
+              // copies into the caller's buffers queued: drain every lane before returning
+        for (int l = 0; l < nl; ++l) hipStreamSynchronize(lanes_[l]->stream);
     for (int i = 0; i < n; ++i)  // the first failing frame's status
         if (fr[i].status) return fr[i].status;
     return st;

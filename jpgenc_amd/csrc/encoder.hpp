@@ -35,11 +35,12 @@ struct FrameDesc {
     int status = 0;
 };
 
-struct KernelTimes {  // milliseconds of the last timed frame (HIP events on the slot stream)
+struct KernelTimes {  // milliseconds of the last timed frame (each kernel's own events, KTimer)
     float fdct = 0, dc_stats = 0, entropy = 0, total = 0;
     double fdct_sum = 0, dc_stats_sum = 0, entropy_sum = 0;  // accumulated since reset
     uint64_t frames = 0;
     uint64_t symbols = 0;  // Huffman-coded symbols of the timed frames
+    double code_sum = 0, pack_sum = 0;  // the entropy stage's code and pack kernels alone
 };
 
 class Encoder {

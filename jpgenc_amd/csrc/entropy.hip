@@ -764,9 +764,11 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a)
 
 // Workgroups: at most kEntropyMaxTilesPerWg tiles each (region size); about 384 in
 // all (1.5 per CU: measured best beside the other lanes) unless overridden.  One segment (restart off):
-// 128-block tiles, at least two per workgroup when the frame has two (so a
-// workgroup's stream holds >= 8 bits: its first and last 8 bits, which the
-// placement reads, are defined).  Restart intervals of R MCUs: segments of bpm*R
+// balanced tiles of <= 128 blocks (tile i of nt is blocks [i*nb/nt, (i+1)*nb/nt), so
+// with nt >= 2 every tile holds >= 64 blocks), one or more per workgroup.  Every block
+// codes >= 2 bits (a DC code and an EOB or AC code, each >= 1 bit), so each
+// workgroup's stream holds >= 128 bits and its first and last 8 bits, which the
+// placement reads, are defined.  Restart intervals of R MCUs: segments of bpm*R
 // blocks (>= 3 blocks, >= 6 bits; each starts byte-aligned), each cut into
 // balanced tiles of <= 128 blocks, a whole number of workgroups per segment.
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override) {
@@ -818,10 +820,9 @@ SegLayout fused_layout(const Geometry& g, uint32_t wgs_override) {
     return L;
 }
 
-hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
+hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tcode, const KTimer* tpack) {
     const uint32_t G = a.seg.grid();
-    hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_timed(tcode, entropy_code_kernel, dim3(G), dim3(kK3Threads), s, a);
     if (e != hipSuccess) return e;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
@@ -833,8 +834,7 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s) {
         b.flags |= kExtPlace;
         if ((e = launch_place(b, G, s)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
-    return hipGetLastError();
+    return launch_timed(tpack, entropy_pack_kernel, dim3(G), dim3(kK3Threads), s, b);
 }
 
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {

@@ -817,29 +817,29 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
 }  // namespace
 
 template <int kYh>
-void launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s) {
+void launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
     const bool ex = a.maxval == 255;
     if (a.solo) {
-        if (ex) hipLaunchKernelGGL((fdct_row8_kernel<true, kK1WavesSolo, kYh>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
-        else hipLaunchKernelGGL((fdct_row8_kernel<false, kK1WavesSolo, kYh>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+        if (ex) (void)launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        else (void)launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
     } else {
-        if (ex) hipLaunchKernelGGL((fdct_row8_kernel<true, kK1WavesShared, kYh>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
-        else hipLaunchKernelGGL((fdct_row8_kernel<false, kK1WavesShared, kYh>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        if (ex) (void)launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        else (void)launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
     }
 }
 
 template <int kFilt>
-void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s) {
+void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
     const bool ex = a.maxval == 255;
     if (a.solo) {
-        if (ex) hipLaunchKernelGGL((fdct_kernel<true, kK1WavesSolo, kFilt>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
-        else hipLaunchKernelGGL((fdct_kernel<false, kK1WavesSolo, kFilt>), dim3(grid), dim3(kK1WavesSolo * 64), 0, s, a);
+        if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        else (void)launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
     } else if (a.fused) {
-        if (ex) hipLaunchKernelGGL((fdct_kernel<true, kK1WavesShared, kFilt, true>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
-        else hipLaunchKernelGGL((fdct_kernel<false, kK1WavesShared, kFilt, true>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt, true>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        else (void)launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt, true>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
     } else {
-        if (ex) hipLaunchKernelGGL((fdct_kernel<true, kK1WavesShared, kFilt>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
-        else hipLaunchKernelGGL((fdct_kernel<false, kK1WavesShared, kFilt>), dim3(grid), dim3(kK1WavesShared * 64), 0, s, a);
+        if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        else (void)launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
     }
 }
 
@@ -852,7 +852,7 @@ uint32_t fdct_grid(const Geometry& g, bool solo) {
     return wgs < cap ? wgs : cap;
 }
 
-hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
+hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
     // 32-bit buffer offsets: the frame's pixels and coefficients must stay below kOob
     // (a 16384^2 frame needs 805 MB of each)
     if ((uint64_t)a.stride * a.g.height >= kOob || (uint64_t)a.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
@@ -860,18 +860,18 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s) {
     // the kernels assume these shapes (kernels.hpp Geometry)
     if (a.g.row8()) {
         switch (a.g.yh) {
-            case 1: if (a.g.bpm != 3) return hipErrorInvalidValue; launch_row8<1>(a, grid, s); break;
-            case 2: if (a.g.bpm != 4) return hipErrorInvalidValue; launch_row8<2>(a, grid, s); break;
-            case 4: if (a.g.bpm != 6) return hipErrorInvalidValue; launch_row8<4>(a, grid, s); break;
+            case 1: if (a.g.bpm != 3) return hipErrorInvalidValue; launch_row8<1>(a, grid, s, t); break;
+            case 2: if (a.g.bpm != 4) return hipErrorInvalidValue; launch_row8<2>(a, grid, s, t); break;
+            case 4: if (a.g.bpm != 6) return hipErrorInvalidValue; launch_row8<4>(a, grid, s, t); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
     if (a.g.yh != 2 || a.g.bpm != 6) return hipErrorInvalidValue;
     switch (a.g.cfilt) {
-        case kFiltS420m: launch_420<kFiltS420m>(a, grid, s); break;
-        case kFiltS420lm: launch_420<kFiltS420lm>(a, grid, s); break;
-        case kFiltS420: launch_420<kFiltS420>(a, grid, s); break;
+        case kFiltS420m: launch_420<kFiltS420m>(a, grid, s, t); break;
+        case kFiltS420lm: launch_420<kFiltS420lm>(a, grid, s, t); break;
+        case kFiltS420: launch_420<kFiltS420>(a, grid, s, t); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

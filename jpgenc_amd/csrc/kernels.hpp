@@ -286,6 +286,14 @@ inline uint32_t entropy_tiles(const Geometry& g) {
 // local offsets, worst case) plus slack, a whole number of 128-byte lines
 constexpr uint64_t kEntropyRegionBytes = (uint64_t)kEntropyMaxTilesPerWg * kEntropyTile * kStageBytesPerBlock + 128;
 
+// Kernel timing (sampled frames only): when given, the launch goes through
+// hipExtLaunchKernel with these events, which the runtime binds to the kernel's own
+// dispatch (its start and end timestamps, the ones rocprofv3 reports), so their
+// elapsed time is the kernel's execution without launch gaps or marker packets.
+struct KTimer {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
 uint32_t fdct_grid(const Geometry& g, bool solo);
 // statistics workgroups: wgs (0: 3 per CU), within the tile-table bound and the tile count
 uint32_t stats_grid(const SegLayout& L, uint32_t wgs = 0);
@@ -299,20 +307,31 @@ inline uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) { return 
 
 inline uint64_t entropy_ubuf_bytes(const SegLayout& L) { return (uint64_t)L.grid() * kEntropyRegionBytes; }
 
-hipError_t launch_fdct(const FdctArgs& a, hipStream_t s);
-hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
-hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s);
+hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t = nullptr);
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t = nullptr);
+hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s, const KTimer* t = nullptr);
 // [4][256] summed counts and keys into (mapped) host memory, then *host_seq = seq
 hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
                               uint64_t seq, hipStream_t s);
 // code + pack kernels (with the placement scan between them when kExtPlace)
-hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s);
+hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* code = nullptr,
+                          const KTimer* pack = nullptr);
 // stripes: code kernel + summary scan; then placement scan + pack kernel
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s);
 hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s);
 // grids above this many workgroups place by a separate scan (each pack workgroup
 // scanning every record would read G^2 records)
 constexpr uint32_t kInlineScanMaxWgs = 1024;
-constexpr uint32_t kPlaceInCodeMaxWgs = 4096;  // grids the last code workgroup places
+// Grids the last code workgroup places (entropy_code_kernel, EntropyArgs::done).
+// Hardware assumption (gfx950), not the HIP memory model's letter: each workgroup
+// publishes its 48-byte record with agent-scope relaxed atomic stores, which gfx950
+// issues write-through (sc1) to the agent's coherence point, waits for their
+// completion (s_waitcnt vmcnt(0)), and only then counts itself with a device atomic
+// performed at that point; the workgroup completing the count takes an agent-scope
+// acquire fence (buffer_inv sc1) before reading every record.  The formal alternative,
+// a release fence per workgroup, writes back the whole L2 (measured 26% slower).
+// Covered by the GPU tests that run multi-lane batches and compare every frame with
+// the oracle (test_gpu_parity.py: placement in code at 1..G workgroups, batches).
+constexpr uint32_t kPlaceInCodeMaxWgs = 4096;
 
 }  // namespace jpge

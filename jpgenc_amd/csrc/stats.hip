@@ -134,7 +134,6 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
     const uint64_t ybase = (uint64_t)mrow0 * yv * ybw;
     const uint64_t cbase = (uint64_t)mrow0 * mw;
     const float inv_bpm = 1.0f / (float)bpm, inv_mw = 1.0f / (float)mw;
-    const float inv_rst = a.rst.mcus ? 1.0f / (float)a.rst.mcus : 0.0f;
     TileRegs<kK2Threads, kK2Blocks> regs;
     regs.init(tid);
     if (t_first < t_last) regs.load(a.coef, fb0, min((int)fnb, kK2Blocks), tid);
@@ -312,9 +311,9 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             {
                 bool reset = false;
                 if (a.rst.mcus && (k == 0 || k >= (int)bpm - 2)) {
-                    uint32_t r;
-                    udiv24(m6 + a.rst.mcu0, a.rst.mcus, inv_rst, r);
-                    reset = r == 0;
+                    // exact 32-bit remainder: MCU numbers reach 2^26 (65535^2 at 4:4:4),
+                    // beyond udiv24's float reciprocal (rare path: interval-boundary blocks)
+                    reset = (m6 + a.rst.mcu0) % a.rst.mcus == 0;
                 }
                 // the predecessor (dc_pred_index): the previous Y slot, 3 blocks back for an
                 // MCU's first Y block, bpm back for chroma; none in the first MCU
@@ -464,15 +463,13 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     return g > need ? g : need;
 }
 
-hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s) {
+hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s, const KTimer* t) {
     if (!a.ntiles) return hipSuccess;
-    hipLaunchKernelGGL(dc_fixup_kernel, dim3((a.ntiles + kFixThreads - 1) / kFixThreads), dim3(kFixThreads), 0, s, a);
-    return hipGetLastError();
+    return launch_timed(t, dc_fixup_kernel, dim3((a.ntiles + kFixThreads - 1) / kFixThreads), dim3(kFixThreads), s, a);
 }
 
-hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(stats_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kK2Threads), 0, s, a);
-    return hipGetLastError();
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
+    return launch_timed(t, stats_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kK2Threads), s, a);
 }
 
 }  // namespace jpge

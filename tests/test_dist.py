@@ -71,6 +71,7 @@ def test_bench_gpus_n_spawns_ranks_without_a_launcher():
     import subprocess
 
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["JPGE_BENCH_DEVICE_COUNT"] = "3"  # (mocked: a node with 3 GPUs)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--workload", "dist-check"],
                        env=env, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -79,6 +80,29 @@ def test_bench_gpus_n_spawns_ranks_without_a_launcher():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 3 and d["value"] == 3.0
     assert d["batch_frames"] == 256.0 and d["rank0_first"] == [0, 3, 6]
+    assert d["devices"] == {"ranks": 3, "devices_visible": 3, "devices_distinct": 3, "ranks_per_device": 1,
+                            "shared": False}
+
+
+@pytest.mark.timeout(150)
+def test_bench_refuses_more_ranks_than_gpus():
+    """--gpus N on a node with fewer than N GPUs refuses (no fake
+    scaling point); --allow-shared-gpu rehearses it and the line says the ranks share."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["JPGE_BENCH_DEVICE_COUNT"] = "1"  # (mocked: one GPU)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "dist-check"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "need 2 GPU(s), this node shows 1" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    r = subprocess.run(cmd + ["--allow-shared-gpu"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["devices"] == {"ranks": 2, "devices_visible": 1, "devices_distinct": 1, "ranks_per_device": 2,
+                            "shared": True}
 
 
 @pytest.mark.timeout(150)
@@ -87,6 +111,7 @@ def test_bench_spawn_propagates_a_failing_rank():
 
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["JPGE_BENCH_FAIL_RANK"] = "1"  # rank 1 exits 3; rank 0 would wait in a barrier forever
+    env["JPGE_BENCH_DEVICE_COUNT"] = "2"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "dist-check"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 3

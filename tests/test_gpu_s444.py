@@ -94,3 +94,32 @@ def test_s444_rejects_bad_mode_and_stripes(enc444):
         enc444.set_subsampling(421)
     with pytest.raises(J.JpgeError):  # (rejected before the pointer is used)
         enc444.stripe_transform(16, 64 * 3, 64, 64, 0, 4)
+
+
+# a single-lane encoder with one tile per entropy workgroup (the 512-group
+# override and JPGE_ENTROPY_WGS), on flat 4:4:4 frames of 129 MCUs (387 blocks: a
+# ragged last tile), where a workgroup's stream is shortest.  Balanced tiles keep
+# every tile >= 64 blocks, so every workgroup codes >= 128 bits.
+@pytest.mark.parametrize("wgs", [0, 4, 512])
+@pytest.mark.parametrize("w,h", [(344, 24), (1032, 8), (8, 1032)])
+def test_s444_single_lane_one_tile_per_workgroup(w, h, wgs):
+    import os
+    old = os.environ.get("JPGE_ENTROPY_WGS")
+    if wgs:
+        os.environ["JPGE_ENTROPY_WGS"] = str(wgs)
+    try:
+        e = J.Encoder(0, lanes=1)
+    finally:
+        if old is None:
+            os.environ.pop("JPGE_ENTROPY_WGS", None)
+        else:
+            os.environ["JPGE_ENTROPY_WGS"] = old
+    try:
+        e.set_subsampling(444)
+        for kind, q in [(2, 50), (2, 90), (0, 90)]:
+            rgb = J.synth_rgb8(3 + w, w, h, kind=kind)
+            assert e.encode(rgb, quality=q) == _oracle.encode(rgb, q, subsampling=444)
+            frames = [rgb, J.synth_rgb8(4 + w, w, h, kind=kind)]
+            assert e.encode_batch(frames, quality=q) == [_oracle.encode(f, q, subsampling=444) for f in frames]
+    finally:
+        e.close()
