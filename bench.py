@@ -825,6 +825,7 @@ def run_frames(args, rank, local, world, pg):
             "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win},
             # host CPU use over the timed region; quota throttling stalls the pipeline
             "host_cpu": host_cpu_use(cg0, cg1, dt),
+            "devices": args.devices,
         }
         if world == 1 and not args.no_cpu_baseline:
             cpu, hashes = cpu_baseline(args)

@@ -34,21 +34,48 @@ constexpr double kCrR = (double).5f, kCrG = (double)-.4186f, kCrB = (double)-.08
 
 // quantize, Coding.hpp:92-94, of the row pass's output o = w * s_u (Dct.hpp:124-131):
 // (int)std::round(o / q) — two correctly rounded fp64 operations, then round half
-// away from zero.  Fast path: r = w * c with c = fl(s_u / q) is within 2^-51 |r| of
-// the reference's quotient fl(fl(w s_u) / q), and |r| < 2^11 (8-bit samples, q >= 1),
-// so the two differ by < 2^-40: unless r lies within 2^-30 of a half-integer, rint(r)
-// (ties-to-even, but r is no tie) is the reference's integer; integer boundaries are
-// harmless (a quotient on either side of k rounds to k either way).  e = r - rint(r)
-// is exact, so a lane near a half-integer is flagged by |e| > 0.5 - 2^-30 and the
-// whole row is redone the reference's way (rare; one branch per row).
-__device__ __forceinline__ int quant_fast(double w, double c, bool& near_half) {
-    const double r = w * c;
-    const double k = __builtin_rint(r);
-    near_half |= __builtin_fabs(r - k) > 0.5 - 0x1p-30;
-    return (int)k;
+// away from zero.  Fast path in one fp64 instruction per coefficient: the exact
+// product x = w * c, c = fl(s_u / q), is within 2^-40 of the reference's quotient
+// fl(fl(w s_u) / q) (|x| < 2^11: 8-bit samples, q >= 1), and
+// y = fma(w, c, 1.5 * 2^36) rounds it once onto the 2^-16 grid, so the low word of y
+// is n = round(x * 2^16) (two's complement, mod 2^32).  With t = n + 0x8001:
+//   - t >> 16 (its high half) is floor(x + 1/2), the reference's integer unless x
+//     lies within 2^-15 of a half-integer — where the reference's quotient could sit
+//     on the other side of it;
+//   - those are exactly the t whose low half is 0, 1 or 2: one 16-bit min over the
+//     row's 8 values finds them, and such a row is redone the reference's way
+//     (quant_exact; rare, one wave-uniform branch per row).
+// Integer boundaries are harmless (a quotient on either side of k rounds to k).
+constexpr double kQuantMagic = 103079215104.0;  // 1.5 * 2^36: ulp 2^-16
+__device__ __forceinline__ uint32_t quant_fix16(double w, double c) {
+    const double y = __builtin_fma(w, c, kQuantMagic);
+    return (uint32_t)__builtin_bit_cast(uint64_t, y) + 0x8001u;
 }
 
 __device__ __forceinline__ int quant_exact(double w, double s, double q) { return (int)round((w * s) / q); }
+
+// One row of 8 quantised coefficients as int16 x 8 (natural order): the fast path,
+// or the reference's two divisions when any lane of the wave has a near-half row.
+// qrow: this lane's 8 quantisers (LDS).
+__device__ __forceinline__ u32x4 quant_row(const double o[8], const double c[8], const double* qrow) {
+    uint32_t t[8];
+    uint16_t m = 0xFFFF;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        t[u] = quant_fix16(o[u], c[u]);
+        m = __builtin_elementwise_min(m, (uint16_t)t[u]);  // v_min_u16 on the low half
+    }
+    if (__builtin_amdgcn_ballot_w64(m <= 2)) {  // wave-uniform: a real branch, not predication
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = (uint32_t)quant_exact(o[u], kS[u], qrow[u]) << 16;
+    }
+    u32x4 pk;  // the high halves, two per word
+    pk.x = __builtin_amdgcn_perm(t[1], t[0], 0x07060302u);
+    pk.y = __builtin_amdgcn_perm(t[3], t[2], 0x07060302u);
+    pk.z = __builtin_amdgcn_perm(t[5], t[4], 0x07060302u);
+    pk.w = __builtin_amdgcn_perm(t[7], t[6], 0x07060302u);
+    return pk;
+}
 
 constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's range
 #ifndef K1_STORE_AUX
@@ -139,6 +166,16 @@ __device__ __forceinline__ double ycc_ref_c(uint32_t p, double scale, double kr,
 __device__ __forceinline__ double ycc_exact_c(uint32_t p, double kr, double kg, double kb) {
     const double r = (double)(p & 0xFF), g = (double)((p >> 8) & 0xFF), b = (double)(p >> 16);
     return __builtin_fma(kb, b, __builtin_fma(kg, g, kr * r));
+}
+
+// v_permlane32_swap on a double pair: lanes 32-63 of a trade places with lanes 0-31
+// of b (a keeps its low half, b its high half).
+__device__ __forceinline__ void swap_halves(double& a, double& b) {
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+    a = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
 }
 
 // The fused symbol pass over one tile (one wave; its quantised rows in cq, block
@@ -413,9 +450,15 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) p[i] = W.rgbx[(yrow0 + i) * kRgbPitch + col];
     };
+    // Exact colour (8-bit input): a Cb lane and its Cr partner 32 lanes up read the same
+    // pixels, so each reads half of them (rows 8h..8h+7, its 4 samples), converts them for
+    // both components, and the pair trades the other component's values (swap_halves).
+    const int crow0 = kExact ? 8 * ccomp : 0;
     auto load_c = [&](uint2 c[16]) {
+        constexpr int n = kExact ? 8 : 16;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] = *reinterpret_cast<const uint2*>(&W.rgbx[i * kRgbPitch + ccol]);
+        for (int i = 0; i < n; ++i)
+            c[i] = *reinterpret_cast<const uint2*>(&W.rgbx[(crow0 + i) * kRgbPitch + ccol]);
     };
     auto load_iq = [&](int qb, double iq[8]) {
 #pragma unroll
@@ -426,34 +469,58 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
         for (int i = 0; i < 8; ++i) x[i] = kExact ? ycc_exact_y(p[i]) : ycc_ref_y(p[i], scale);
     };
     auto c_inputs = [&](const uint2 c[16], double x[8]) {
+        if constexpr (kExact) {
+            // channel sums of this lane's 4 samples (exact integers), then both components:
+            // the chroma of 8-bit input is exact, and each filter's
+            // 1/4, 1/2 or 1 is folded into the constants (every product stays exact):
+            //   S420_m  ((a+b)+(c+d))/4 of the 2x2 pixels, Image.cpp:207-224;
+            //   S420_lm (a+c)/2 of the two rows' left pixels, Image.cpp:218-224, 297-306;
+            //   S420    the top-left pixel (the masks' zero terms add zeros), Image.cpp:279-286
+            constexpr double f = kFilt == kFiltS420 ? 1.0 : kFilt == kFiltS420lm ? 0.5 : 0.25;
+            double vb[4], vr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint2 t0 = c[2 * i], t1 = c[2 * i + 1];
+                uint32_t sr = t0.x & 0xFF, sg = (t0.x >> 8) & 0xFF, sb = t0.x >> 16;
+                if (kFilt != kFiltS420) {
+                    sr += t1.x & 0xFF;
+                    sg += (t1.x >> 8) & 0xFF;
+                    sb += t1.x >> 16;
+                }
+                if (kFilt == kFiltS420m) {
+                    sr += (t0.y & 0xFF) + (t1.y & 0xFF);
+                    sg += ((t0.y >> 8) & 0xFF) + ((t1.y >> 8) & 0xFF);
+                    sb += (t0.y >> 16) + (t1.y >> 16);
+                }
+                const double dr = (double)sr, dg = (double)sg, db = (double)sb;
+                vb[i] = __builtin_fma(kCbB * f, db, __builtin_fma(kCbG * f, dg, (kCbR * f) * dr));
+                vr[i] = __builtin_fma(kCrB * f, db, __builtin_fma(kCrG * f, dg, (kCrR * f) * dr));
+            }
+            // lanes < 32 (Cb) keep Cb of samples 0-3 and receive Cb of 4-7; lanes >= 32 (Cr)
+            // receive Cr of 0-3 and keep Cr of 4-7
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                swap_halves(vb[i], vr[i]);
+                x[i] = vb[i];
+                x[4 + i] = vr[i];
+            }
+            return;
+        }
         const double kr = ccomp ? kCrR : kCbR, kg = ccomp ? kCrG : kCbG, kb = ccomp ? kCrB : kCbB;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint2 t0 = c[2 * i], t1 = c[2 * i + 1];
+            // other maxvals: the reference's per-pixel op order
             if (kFilt == kFiltS420) {
                 // subsample(S420), Image.cpp:279-286: mask {1, 0} on even rows only, the
                 // top-left sample (the mask's 0 * b adds a zero)
-                x[i] = kExact ? ycc_exact_c(t0.x, kr, kg, kb) : ycc_ref_c(t0.x, scale, kr, kg, kb);
+                x[i] = ycc_ref_c(t0.x, scale, kr, kg, kb);
             } else if (kFilt == kFiltS420lm) {
                 // subsample(S420_lm), Image.cpp:297-306, 218-224: (a + c) / 2 of the left
-                // samples of both rows; exact for 8-bit input, as the channel sums
-                if (kExact) {
-                    const uint32_t rb = (t0.x & 0xFF00FFu) + (t1.x & 0xFF00FFu), all = t0.x + t1.x;
-                    const double sr = (double)(rb & 0xFFFF), sb = (double)(rb >> 16), sg = (double)((all - rb) >> 8);
-                    x[i] = __builtin_fma(kb * 0.5, sb, __builtin_fma(kg * 0.5, sg, (kr * 0.5) * sr));
-                } else {
-                    double v = ycc_ref_c(t0.x, scale, kr, kg, kb);
-                    v += ycc_ref_c(t1.x, scale, kr, kg, kb);
-                    x[i] = v / 2;
-                }
-            } else if (kExact) {
-                // ((a+b)+(c+d))/4 of the exact per-pixel values equals the exact value
-                // of the channel sums
-                const uint32_t rb = (t0.x & 0xFF00FFu) + (t0.y & 0xFF00FFu) + (t1.x & 0xFF00FFu) + (t1.y & 0xFF00FFu);
-                const uint32_t all = t0.x + t0.y + t1.x + t1.y;  // fields overlap; G = (all - rb) >> 8
-                const double sr = (double)(rb & 0xFFFF), sb = (double)(rb >> 16), sg = (double)((all - rb) >> 8);
-                // (the 1/4 is folded into the constants: every product stays exact)
-                x[i] = __builtin_fma(kb * 0.25, sb, __builtin_fma(kg * 0.25, sg, (kr * 0.25) * sr));
+                // samples of both rows
+                double v = ycc_ref_c(t0.x, scale, kr, kg, kb);
+                v += ycc_ref_c(t1.x, scale, kr, kg, kb);
+                x[i] = v / 2;
             } else {
                 // subsample(S420_m), Image.cpp:207-224: ((0+a+b) + (0+c+d)) / 4
                 double top = 0.0, bot = 0.0;
@@ -534,20 +601,9 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
             wave_order();
             prefetch_next();  // next round's inputs: after this round's LDS reads
             arai8_unscaled(x, o);  // y(j, u) = o[u] * s_u
-            int qv[8];
-            bool near_half = false;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) qv[u] = quant_fast(o[u], iqc[u], near_half);
-            if (__builtin_amdgcn_ballot_w64(near_half)) {  // wave-uniform: a real branch, not predication
-#pragma unroll
-                for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], kS[u], lds.q[qb][j * kQRow + u]);
-            }
+            pk = quant_row(o, iqc, &lds.q[qb][j * kQRow]);
             const uint32_t blk = (mrow * mw + mcol0 + m) * 6 + slot;
             off = (!kFused && m < nvalid) ? blk * 128 + j * 16 : kOob;
-            pk.x = __builtin_amdgcn_perm((uint32_t)qv[1], (uint32_t)qv[0], 0x05040100u);
-            pk.y = __builtin_amdgcn_perm((uint32_t)qv[3], (uint32_t)qv[2], 0x05040100u);
-            pk.z = __builtin_amdgcn_perm((uint32_t)qv[5], (uint32_t)qv[4], 0x05040100u);
-            pk.w = __builtin_amdgcn_perm((uint32_t)qv[7], (uint32_t)qv[6], 0x05040100u);
             if constexpr (kFused) {  // the row to the tile's LDS copy (no coefficient store)
                 if (m < nvalid) lds.fx.cq[wv][(m * 6 + slot) * 8 + j] = make_uint4(pk.x, pk.y, pk.z, pk.w);
             }
@@ -783,21 +839,9 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
                 if (round == 1) load_iq(1, iq);
             }
             arai8_unscaled(x, o);
-            int qv[8];
-            bool near_half = false;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) qv[u] = quant_fast(o[u], iqc[u], near_half);
-            if (__builtin_amdgcn_ballot_w64(near_half)) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) qv[u] = quant_exact(o[u], kS[u], lds.q[qb][j * kQRow + u]);
-            }
+            const u32x4 pk = quant_row(o, iqc, &lds.q[qb][j * kQRow]);
             const uint32_t blk = (mrow * mw + mcol0 + m) * kBpm + slot;
             const uint32_t off = m < nvalid ? blk * 128 + j * 16 : kOob;
-            u32x4 pk;
-            pk.x = __builtin_amdgcn_perm((uint32_t)qv[1], (uint32_t)qv[0], 0x05040100u);
-            pk.y = __builtin_amdgcn_perm((uint32_t)qv[3], (uint32_t)qv[2], 0x05040100u);
-            pk.z = __builtin_amdgcn_perm((uint32_t)qv[5], (uint32_t)qv[4], 0x05040100u);
-            pk.w = __builtin_amdgcn_perm((uint32_t)qv[7], (uint32_t)qv[6], 0x05040100u);
             if (round < kRounds - 1) {
                 __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
             } else {
