@@ -168,6 +168,26 @@ __device__ __forceinline__ double ycc_exact_c(uint32_t p, double kr, double kg, 
     return __builtin_fma(kb, b, __builtin_fma(kg, g, kr * r));
 }
 
+// The prologue reads its constants without vector loads: a vector load issued after
+// the first tile's pixel loads waits for them (the vector memory counter retires in
+// order), which held every workgroup's prologue for the start-up burst (~3.5 us).
+// kS[u] as a select over the constants (no load from the constant table):
+__device__ __forceinline__ double arai_scale(int u) {
+    double r = kS[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) r = u == i ? kS[i] : r;
+    return r;
+}
+// quantiser entry tid (< 128) of the kernel arguments, through scalar loads (the
+// array is 16-byte aligned in FdctArgs):
+__device__ __forceinline__ uint32_t q_entry(const FdctArgs& a, int tid) {
+    const uint32_t* qw = reinterpret_cast<const uint32_t*>(a.q);
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) w = (tid >> 2) == i ? qw[i] : w;
+    return (w >> (8 * (tid & 3))) & 0xFF;
+}
+
 // v_permlane32_swap on a double pair: lanes 32-63 of a trade places with lanes 0-31
 // of b (a keeps its low half, b its high half).
 __device__ __forceinline__ void swap_halves(double& a, double& b) {
@@ -420,9 +440,9 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     if (tid == 0) lds.next = kWaves;
     if (tid < 128) {
         const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
-        const double q = (double)a.q[tid];  // Image.cpp:611-636 divides by the entry as double
+        const double q = (double)q_entry(a, tid);  // Image.cpp:611-636 divides by the entry as double
         lds.q[c][o] = q;
-        lds.invq[c][o] = kS[e & 7] / q;
+        lds.invq[c][o] = arai_scale(e & 7) / q;
     }
     if constexpr (kFused) {
         for (int i = tid; i < kFHistCopies * kFCopyWords; i += kK1Threads) (&lds.fx.acnt[0][0])[i] = 0;
@@ -433,7 +453,9 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     // row, chroma raster index of that MCU row (keys are relative to them, as in K2)
     const uint32_t mrow0 = tb_p / tiles_per_row;
     const uint32_t ybase = mrow0 * 4 * mw, cbase = mrow0 * mw;
-    __syncthreads();
+    // LDS-only barrier: the prologue's shared state is in LDS (a full __syncthreads
+    // would also wait for the first tile's pixels, issued above)
+    lds_barrier();
     JPGE_STAMP(0);
     uint32_t kn = k < n_p ? grab() : n_p;  // the next tile (its pixels are prefetched a tile ahead)
 
@@ -739,11 +761,13 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
     if (tid == 0) lds.next = kWaves;
     if (tid < 128) {
         const int c = tid >> 6, e = tid & 63, o = (e >> 3) * kQRow + (e & 7);
-        const double q = (double)a.q[tid];
+        const double q = (double)q_entry(a, tid);
         lds.q[c][o] = q;
-        lds.invq[c][o] = kS[e & 7] / q;
+        lds.invq[c][o] = arai_scale(e & 7) / q;
     }
-    __syncthreads();
+    // LDS-only barrier: the prologue's shared state is in LDS (a full __syncthreads
+    // would also wait for the first tile's pixels, issued above)
+    lds_barrier();
     JPGE_STAMP(0);
     uint32_t kn = k < n_p ? grab() : n_p;
 

@@ -73,7 +73,9 @@ struct FdctArgs {
     Geometry g;
     int maxval;      // 255 -> exact integer colour path
     bool solo;       // the kernel has the GPU to itself: whole-CU workgroups (else 4-wave ones)
-    uint8_t q[128];  // luma then chroma quantisers, natural order (bytes: a small kernarg block)
+    // luma then chroma quantisers, natural order (bytes: a small kernarg block; 16-byte
+    // aligned so the kernels fetch it with scalar loads, see fdct.hip q_entry)
+    alignas(16) uint8_t q[128];
     int16_t* coef;
     uint32_t* zero;       // the frame's control block, zeroed by this kernel (it runs first)
     uint32_t zero_words;

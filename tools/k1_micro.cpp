@@ -79,22 +79,43 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    // kernel-exact times of every timed launch (events bound to the dispatch, KTimer)
+    std::vector<hipEvent_t> kev(2 * iters * nf);
+    for (auto& e : kev) CK(hipEventCreate(&e));
+    int kn = -1;
     auto run = [&](int f) {
         a.rgb = rgb + fbytes * f;
         a.coef = coef + (cbytes / 2) * f;
-        CK(jpge::launch_fdct(a, 0));
+        jpge::KTimer t{};
+        if (kn >= 0) t = jpge::KTimer{kev[2 * kn], kev[2 * kn + 1]}, ++kn;
+        CK(jpge::launch_fdct(a, 0, kn >= 0 ? &t : nullptr));
     };
     for (int w = 0; w < 3; ++w)
         for (int f = 0; f < nf; ++f) run(f);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, 0));
+    kn = 0;
     for (int it = 0; it < iters; ++it)
         for (int f = 0; f < nf; ++f) run(f);
+    kn = -1;
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = 1000.0 * ms / (iters * nf);
+    {
+        std::vector<double> k;
+        for (int i = 0; i < iters * nf; ++i) {
+            float m;
+            CK(hipEventElapsedTime(&m, kev[2 * i], kev[2 * i + 1]));
+            k.push_back(1000.0 * m);
+        }
+        std::sort(k.begin(), k.end());
+        double sum = 0;
+        for (double v : k) sum += v;
+        std::printf("kernel-exact: mean %.2f us  min %.2f  median %.2f  max %.2f\n", sum / k.size(), k[0],
+                    k[k.size() / 2], k.back());
+    }
 #ifdef JPGE_STAMPS
     {  // per-workgroup phase stamps of one more launch (s_memrealtime, 100 MHz)
         const uint32_t G = jpge::fdct_grid(g, a.solo);
