@@ -22,8 +22,9 @@ DEV_OBJS  := $(addprefix $(BUILD)/,$(DEV_SRCS:.hip=.o))
 DIAG_OBJS := $(addprefix $(BUILD)/diag/,$(DEV_SRCS:.hip=.o))
 HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h
 FACADE_TEST := tests/cpp/bin/test_facade
+HUFF_TEST   := tests/cpp/bin/test_huffman_fast
 
-all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) oracle
+all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) $(HUFF_TEST) oracle
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HEADERS)
 	@mkdir -p $(BUILD)
@@ -68,3 +69,9 @@ $(FACADE_TEST): tests/cpp/test_facade.cpp $(LIBDIR)/libjpge.so $(SRC)/jpge_image
 	@mkdir -p tests/cpp/bin
 	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -ljpge -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' \
 	  -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+
+# the Huffman table builder's array emulation against the standard containers
+# (tests/test_host.py runs it)
+$(HUFF_TEST): tests/cpp/test_huffman_fast.cpp $(SRC)/huffman.cpp $(SRC)/huffman.hpp
+	@mkdir -p tests/cpp/bin
+	$(CXX) $(CXXFLAGS) -o $@ $< $(SRC)/huffman.cpp

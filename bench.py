@@ -299,6 +299,40 @@ def thread_cpu() -> dict:
     return out
 
 
+class ThreadSampler:
+    """Diagnostic (JPGE_BENCH_THREADS): samples every thread's scheduler state and
+    kernel wait channel every 2 ms; stop() prints each busy thread's distribution."""
+
+    def __init__(self):
+        import threading
+
+        self.counts = collections.defaultdict(collections.Counter)
+        self.done = threading.Event()
+        self.th = threading.Thread(target=self.run, daemon=True)
+        self.th.start()
+
+    def run(self):
+        while not self.done.wait(0.002):
+            for tid in os.listdir("/proc/self/task"):
+                try:
+                    with open(f"/proc/self/task/{tid}/stat") as f:
+                        st = f.read()
+                    with open(f"/proc/self/task/{tid}/wchan") as f:
+                        wc = f.read().strip() or "0"
+                    name = st[st.index("(") + 1:st.rindex(")")]
+                    state = st[st.rindex(")") + 2]
+                    self.counts[f"{name}/{tid}"][f"{state}:{wc}"] += 1
+                except (OSError, ValueError):
+                    pass
+
+    def stop(self):
+        self.done.set()
+        self.th.join()
+        for k, c in self.counts.items():
+            if sum(n for s, n in c.items() if s.startswith("R")) > 0:
+                print(f"sampler {k}: {dict(c.most_common(6))}", file=sys.stderr)
+
+
 def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
     """Per-launch HBM bytes per stage from the newest committed rocprofv3 PMC summary of this
     frame size (profiles/pmc_rNN.json for 4K, profiles/rNN_pmc_<size>.json for others; the
@@ -633,6 +667,7 @@ def run_frames(args, rank, local, world, pg):
     step_t = []
     cg0 = cgroup_cpu_stat()
     th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
+    sampler = ThreadSampler() if th0 else None
     for _ in range(args.steps):
         ts = time.perf_counter()
         lens = enc.encode_batch_dev(frames, outd, quality=args.quality)
@@ -643,6 +678,8 @@ def run_frames(args, rank, local, world, pg):
     dt = time.perf_counter() - t0
     win1 = time.monotonic_ns()
     cg1 = cgroup_cpu_stat()
+    if sampler:
+        sampler.stop()
     if th0:
         th1 = thread_cpu()
         use = collections.Counter()

@@ -73,8 +73,9 @@ inline hipError_t wait_event(hipEvent_t e) {
 // which costs the GPU ~6 us of idle each time.  `queued`: set once the kernel that
 // writes the word is on the stream (another thread launches it); before that an
 // idle stream is no error.
-inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool nap = false,
+inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int nap_us = 0,
                     const std::atomic<int>* queued = nullptr) {
+    const bool nap = nap_us > 0;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto next_query = t0 + std::chrono::milliseconds(2);
@@ -82,7 +83,7 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, bool
     bool idle = false;
     for (uint32_t spins = 0;; ++spins) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return kOk;
-        if (nap) std::this_thread::sleep_for(std::chrono::microseconds(10));
+        if (nap) std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
         if (!nap && (spins & 255) != 255) continue;
         const auto now = clk::now();
         if (now < next_query) continue;
@@ -381,6 +382,8 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
+    e->inline_tables_ = env_int("JPGE_INLINE_TABLES", 1, 0, 1) != 0;
+    e->nap_us_ = env_int("JPGE_NAP_US", e->nap_us_, 1, 1000);
     const int nap = env_int("JPGE_NAP", -1, -1, 1);
     e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
     e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
@@ -696,7 +699,8 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel) {
-    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, /*nap=*/!parallel, &s.export_queued)) return w;
+    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : 10), &s.export_queued))
+        return w;
     uint32_t cnt[1024];
     uint64_t first[1024];
     for (int i = 0; i < 1024; ++i) {
@@ -766,7 +770,7 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
 }
 
 int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
-    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_)) return w;
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[7]));
         std::lock_guard<std::mutex> g(times_mu_);
@@ -822,7 +826,7 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
-    if (!pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
+    if (!inline_tables_ && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
     // Frames are dealt dynamically: a lane takes the batch's next frame when its
     // pipeline has room, so lanes finish together.  Lane 0 runs on the calling thread.
     const int nl = std::min<int>((int)lanes_.size(), n);
@@ -881,7 +885,11 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
     // pipeline's edges fall back to a standalone export kernel and a table copy.
     const int L = lookahead_, D = drain_lag_;
     auto submit_tables = [&](Slot& s) {
-        if (pool_) {
+        if (inline_tables_) {
+            // built by this lane's thread when the frame's entropy launch needs them
+            // (below): no pool workers polling for histograms, no hand-off
+            s.tables_done.store(0, std::memory_order_relaxed);
+        } else if (pool_) {
             Slot* sp = &s;
             const int dev = device_;
             // ready once the histograms are in (or after 2 ms, when build_tables'
@@ -935,8 +943,12 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         Slot* sj = nullptr;  // frame j, tables built, ready for its entropy kernels
         if (j >= 0 && j < n && !frame(j).status) {
             Slot& s = *ln.slots[j % S];
+            if (inline_tables_ && !s.tables_done.load(std::memory_order_acquire)) {
+                s.tables_status = build_tables(s, false);
+                s.tables_done.store(1, std::memory_order_release);
+            }
             while (!s.tables_done.load(std::memory_order_acquire)) {
-                if (nap_) std::this_thread::sleep_for(std::chrono::microseconds(10));
+                if (nap_) std::this_thread::sleep_for(std::chrono::microseconds(nap_us_));
                 else std::this_thread::yield();
             }
             if (s.tables_status) note(j, s.tables_status);

@@ -167,7 +167,9 @@ class Encoder {
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
-    int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables
+    int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables (JPGE_INLINE_TABLES=0)
+    bool inline_tables_ = true; // JPGE_INLINE_TABLES: each lane's thread builds its frames' tables (no pool)
+    int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
     // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
     // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
     // lanes (one small launch instead of every pack workgroup scanning all records:

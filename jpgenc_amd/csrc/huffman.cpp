@@ -1,6 +1,8 @@
 #include "huffman.hpp"
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <numeric>
 #include <queue>
 #include <unordered_map>
@@ -24,8 +26,8 @@ using Level = std::priority_queue<Item, std::vector<Item>, ItemGreater>;
 
 }  // namespace
 
-void build_code_lengths(const std::vector<std::pair<int, int>>& first_order_counts,
-                        std::vector<std::vector<int>>& by_len) {
+void build_code_lengths_std(const std::vector<std::pair<int, int>>& first_order_counts,
+                            std::vector<std::vector<int>>& by_len) {
     // symbol_counts (Huffman.cpp:6-9): insertion in first-occurrence order; the
     // map's iteration order then gives the Symbol vector order (:11-14).
     std::unordered_map<int, int> counts;
@@ -120,6 +122,247 @@ void build_code_lengths(const std::vector<std::pair<int, int>>& first_order_coun
     by_len[last + 1].push_back(s);
 }
 
+// ---- the same algorithm without standard containers (the per-frame hot path) ----
+//
+// build_code_lengths_std above feeds std::unordered_map and std::priority_queue; the
+// code below reproduces what those containers do, step for step, on fixed arrays:
+//  - HashOrder: the iteration order of a libstdc++ std::unordered_map<int, int> after
+//    inserting keys in a given order (hash = identity; a new key goes to the front of
+//    its bucket, or of the whole list when its bucket is empty; a rehash relinks the
+//    list in the same way), with the bucket counts recorded once from a real map;
+//  - the binary heap of std::priority_queue<Item, vector<Item>, ItemGreater>: push =
+//    std::push_heap, pop = std::pop_heap (libstdc++'s __adjust_heap, then __push_heap),
+//    comparing weights only;
+//  - packages as a DAG of node ids: a symbol's code length is its number of paths
+//    from the final packages (Huffman.hpp:153-161), and code_lengths receives the
+//    symbols by (first final package that holds them, symbol), as std::merge keeps a
+//    package's symbols sorted (Huffman.hpp:103-108).
+// tests/cpp/test_huffman_fast.cpp checks it against build_code_lengths_std and
+// std::unordered_map on random inputs; the package-merge golden cases pin both.
+namespace {
+
+constexpr int kMaxSyms = 256;
+
+class HashOrder {
+  public:
+    // bucket_count() of a std::unordered_map<int, int> after k insertions (k <= kMaxSyms)
+    static const uint32_t* buckets() {
+        static const std::vector<uint32_t> bc = [] {
+            std::vector<uint32_t> v(kMaxSyms + 1);
+            std::unordered_map<int, int> m;
+            v[0] = (uint32_t)m.bucket_count();
+            for (int k = 1; k <= kMaxSyms; ++k) {
+                m.emplace(k, k);
+                v[k] = (uint32_t)m.bucket_count();
+            }
+            return v;
+        }();
+        return bc.data();
+    }
+    // iteration order (indices into keys) after inserting distinct keys[0..n) (std::hash<int>:
+    // the value as size_t, so a negative key hashes to 2^64 + key)
+    static void order(const int* keys, int n, int* out) {
+        constexpr int kNone = -1, kBefore = -2;  // bucket empty / its predecessor is before_begin
+        const uint32_t* bc = buckets();
+        int next[kMaxSyms];
+        int bucket[kMaxSyms + 64];  // node before the bucket's first node
+        uint32_t nb = bc[0];
+        int head = kNone;
+        for (uint32_t b = 0; b < nb; ++b) bucket[b] = kNone;
+        for (int i = 0; i < n; ++i) {
+            if (bc[i + 1] != nb) {  // _M_rehash_aux (unique keys)
+                nb = bc[i + 1];
+                for (uint32_t b = 0; b < nb; ++b) bucket[b] = kNone;
+                int p = head, bbegin = 0;
+                head = kNone;
+                while (p != kNone) {
+                    const int nx = next[p];
+                    const uint32_t b = (uint32_t)(static_cast<size_t>(keys[p]) % nb);
+                    if (bucket[b] == kNone) {
+                        next[p] = head;
+                        head = p;
+                        bucket[b] = kBefore;
+                        if (next[p] != kNone) bucket[bbegin] = p;
+                        bbegin = (int)b;
+                    } else if (bucket[b] == kBefore) {
+                        next[p] = head;
+                        head = p;
+                    } else {
+                        next[p] = next[bucket[b]];
+                        next[bucket[b]] = p;
+                    }
+                    p = nx;
+                }
+            }
+            const uint32_t b = (uint32_t)(static_cast<size_t>(keys[i]) % nb);  // _M_insert_bucket_begin
+            if (bucket[b] != kNone) {
+                if (bucket[b] == kBefore) {
+                    next[i] = head;
+                    head = i;
+                } else {
+                    next[i] = next[bucket[b]];
+                    next[bucket[b]] = i;
+                }
+            } else {
+                next[i] = head;
+                head = i;
+                if (next[i] != kNone) bucket[static_cast<size_t>(keys[next[i]]) % nb] = i;
+                bucket[b] = kBefore;
+            }
+        }
+        int k = 0;
+        for (int p = head; p != kNone; p = next[p]) out[k++] = p;
+    }
+};
+
+struct HeapItem {
+    int w;
+    int node;
+};
+// std::push_heap with comp(a, b) = a.w > b.w (libstdc++ __push_heap)
+inline void heap_push(HeapItem* h, int& size, HeapItem v) {
+    int hole = size++;
+    int parent = (hole - 1) / 2;
+    while (hole > 0 && h[parent].w > v.w) {
+        h[hole] = h[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    h[hole] = v;
+}
+// std::pop_heap + pop_back (libstdc++ __pop_heap / __adjust_heap / __push_heap)
+inline HeapItem heap_pop(HeapItem* h, int& size) {
+    const HeapItem top = h[0];
+    const int len = size - 1;
+    if (len > 0) {
+        const HeapItem v = h[len];
+        int hole = 0, child = 0;
+        while (child < (len - 1) / 2) {
+            child = 2 * (child + 1);
+            if (h[child].w > h[child - 1].w) --child;
+            h[hole] = h[child];
+            hole = child;
+        }
+        if ((len & 1) == 0 && child == (len - 2) / 2) {
+            child = 2 * (child + 1);
+            h[hole] = h[child - 1];
+            hole = child - 1;
+        }
+        int parent = (hole - 1) / 2;
+        while (hole > 0 && h[parent].w > v.w) {
+            h[hole] = h[parent];
+            hole = parent;
+            parent = (hole - 1) / 2;
+        }
+        h[hole] = v;
+    }
+    size = len;
+    return top;
+}
+
+// by_len[l] = the symbols of code length l (l = 1..17) in the reference's order;
+// syms/cnts: the distinct symbols and counts in first-occurrence order.
+void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][kMaxSyms], int nlen[18]) {
+    for (int l = 0; l < 18; ++l) nlen[l] = 0;
+    if (n <= 0) return;
+    // leaves in the iteration order of symbol_counts (Huffman.cpp:6-14)
+    int ord[kMaxSyms], lsym[kMaxSyms], lcnt[kMaxSyms];
+    HashOrder::order(syms, n, ord);
+    for (int i = 0; i < n; ++i) {
+        lsym[i] = syms[ord[i]];
+        lcnt[i] = cnts[ord[i]];
+    }
+    if (n == 1) {  // Huffman.cpp:17-25
+        by_len[1][nlen[1]++] = lsym[0];
+        return;
+    }
+    // package-merge, Huffman.hpp:114-174: 15 levels, each a copy of the leaves' heap
+    // plus the previous level's packages; levels[15] starts empty
+    constexpr int kLevels = 15, kCap = 2 * kMaxSyms;
+    HeapItem base[kMaxSyms], cur[kCap], nxt[kCap];
+    int nbase = 0;
+    for (int i = 0; i < n; ++i) heap_push(base, nbase, HeapItem{lcnt[i], i});
+    static thread_local std::vector<std::pair<int, int>> kids;
+    kids.clear();
+    int ncur = nbase;
+    std::copy(base, base + nbase, cur);
+    for (int lv = 0; lv < kLevels; ++lv) {
+        int nn = 0;
+        if (lv + 1 < kLevels) {
+            std::copy(base, base + nbase, nxt);
+            nn = nbase;
+        }
+        while (ncur > 1) {
+            const HeapItem a = heap_pop(cur, ncur), b = heap_pop(cur, ncur);
+            kids.emplace_back(a.node, b.node);
+            heap_push(nxt, nn, HeapItem{a.w + b.w, n + (int)kids.size() - 1});
+        }
+        std::copy(nxt, nxt + nn, cur);
+        ncur = nn;
+    }
+    // cur: levels[15]; pop order = the final packages.  Push the multiplicities and the
+    // first final package down the DAG (a package's id exceeds its children's).
+    const int total = n + (int)kids.size();
+    static thread_local std::vector<int> mult, first;
+    mult.assign(total, 0);
+    first.assign(total, INT32_MAX);
+    for (int k = 0; ncur > 0; ++k) {
+        const int f = heap_pop(cur, ncur).node;
+        mult[f] += 1;
+        if (k < first[f]) first[f] = k;
+    }
+    for (int id = total - 1; id >= n; --id) {
+        if (!mult[id]) continue;
+        const auto& kk = kids[id - n];
+        mult[kk.first] += mult[id];
+        mult[kk.second] += mult[id];
+        if (first[id] < first[kk.first]) first[kk.first] = first[id];
+        if (first[id] < first[kk.second]) first[kk.second] = first[id];
+    }
+    // code_lengths (an unordered_map) receives symbols by (first package, symbol)
+    int ins[kMaxSyms];
+    for (int i = 0; i < n; ++i) ins[i] = i;
+    std::sort(ins, ins + n, [&](int x, int y) {
+        return first[x] != first[y] ? first[x] < first[y] : lsym[x] < lsym[y];
+    });
+    int ksym[kMaxSyms];
+    for (int i = 0; i < n; ++i) ksym[i] = lsym[ins[i]];
+    HashOrder::order(ksym, n, ord);
+    for (int i = 0; i < n; ++i) {
+        const int leaf = ins[ord[i]], l = mult[leaf];
+        by_len[l][nlen[l]++] = lsym[leaf];
+    }
+    // preventOnlyOnesCode (Huffman.cpp:37-48): the last symbol of the longest length
+    // moves one level deeper
+    int last = 16;
+    while (last > 0 && nlen[last] == 0) --last;
+    const int sv = by_len[last][--nlen[last]];
+    by_len[last + 1][nlen[last + 1]++] = sv;
+}
+
+}  // namespace
+
+void build_code_lengths(const std::vector<std::pair<int, int>>& first_order_counts,
+                        std::vector<std::vector<int>>& by_len) {
+    const int n = (int)first_order_counts.size();
+    if (n > kMaxSyms) {  // (symbol texts beyond byte symbols: the facade only)
+        build_code_lengths_std(first_order_counts, by_len);
+        return;
+    }
+    by_len.assign(17, {});
+    if (n == 0) return;
+    int syms[kMaxSyms], cnts[kMaxSyms];
+    for (int i = 0; i < n; ++i) {
+        syms[i] = first_order_counts[i].first;
+        cnts[i] = first_order_counts[i].second;
+    }
+    static thread_local int bl[18][kMaxSyms];
+    int nl[18];
+    code_lengths_fast(syms, cnts, n, bl, nl);
+    by_len.assign(17, {});  // (lengths <= 16: package-merge limits them to 15, +1 for preventOnlyOnesCode)
+    for (int l = 0; l < 17; ++l) by_len[l].assign(bl[l], bl[l] + nl[l]);
+}
+
 std::vector<std::pair<int, GenericCode>> assign_codes(const std::vector<std::vector<int>>& by_len) {
     // generateCodes (Huffman.cpp:50-66): canonical codes in SymbolsPerLength order.
     std::vector<std::pair<int, GenericCode>> out;
@@ -131,7 +374,8 @@ std::vector<std::pair<int, GenericCode>> assign_codes(const std::vector<std::vec
     return out;
 }
 
-bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out) {
+static bool build_table_with(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out,
+                             void (*lengths)(const std::vector<std::pair<int, int>>&, std::vector<std::vector<int>>&)) {
     std::vector<std::pair<uint64_t, int>> order;
     for (int s = 0; s < 256; ++s)
         if (counts[s]) order.emplace_back(first_key[s], s);
@@ -142,7 +386,7 @@ bool build_table(const uint32_t counts[256], const uint64_t first_key[256], Huff
     for (const auto& o : order) fc.emplace_back(o.second, (int)counts[o.second]);
 
     std::vector<std::vector<int>> by_len;
-    build_code_lengths(fc, by_len);
+    lengths(fc, by_len);
     out = HuffTable();
     int k = 0;
     for (int l = 1; l <= 16 && l < (int)by_len.size(); ++l) {
@@ -154,6 +398,45 @@ bool build_table(const uint32_t counts[256], const uint64_t first_key[256], Huff
         out.code[sc.first & 0xFF] = sc.second.code;
         out.len[sc.first & 0xFF] = (uint8_t)sc.second.length;
     }
+    return true;
+}
+
+bool build_table_std(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out) {
+    return build_table_with(counts, first_key, out, build_code_lengths_std);
+}
+
+bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out) {
+    // symbols in first-occurrence order
+    uint64_t key[kMaxSyms];
+    int syms[kMaxSyms], cnts[kMaxSyms], n = 0;
+    for (int s = 0; s < 256; ++s)
+        if (counts[s]) {
+            key[n] = (first_key[s] << 8) | (uint64_t)s;  // (keys are < 2^56: text positions)
+            ++n;
+        }
+    if (!n) return false;
+    std::sort(key, key + n);
+    for (int i = 0; i < n; ++i) {
+        syms[i] = (int)(key[i] & 0xFF);
+        cnts[i] = (int)counts[syms[i]];
+    }
+    int bl[18][kMaxSyms], nl[18];
+    code_lengths_fast(syms, cnts, n, bl, nl);
+    out = HuffTable();
+    // canonical codes in SymbolsPerLength order (generateCodes, Huffman.cpp:50-66)
+    int k = 0;
+    uint32_t c = 0;
+    for (int l = 1; l < 18; ++l) {
+        if (l <= 16) out.bits[l] = (uint8_t)nl[l];
+        for (int i = 0; i < nl[l]; ++i) {
+            const int sv = bl[l][i];
+            if (l <= 16) out.huffval[k++] = (uint8_t)sv;
+            out.code[sv & 0xFF] = c++;
+            out.len[sv & 0xFF] = (uint8_t)l;
+        }
+        c <<= 1;
+    }
+    out.nsym = k;
     return true;
 }
 

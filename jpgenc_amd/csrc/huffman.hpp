@@ -39,6 +39,11 @@ std::vector<std::pair<int, GenericCode>> assign_codes(const std::vector<std::vec
 // (keys are any totally ordered u64; absent symbols have counts[s] == 0).
 // Returns false if every count is zero.
 bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out);
+// The same table through std::unordered_map / std::priority_queue themselves (the
+// containers the reference uses; test cross-check of build_table's array emulation).
+bool build_table_std(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out);
+void build_code_lengths_std(const std::vector<std::pair<int, int>>& first_order_counts,
+                            std::vector<std::vector<int>>& by_len);
 
 // Facade mirror of the reference entry point (Huffman.hpp:53): a symbol text in,
 // (symbol -> code) and SymbolsPerLength out.

@@ -139,3 +139,17 @@ def test_quality_tables_match_oracle_every_q():
         qy, qc = J.quality_tables(q)
         oy, oc = _oracle.quality_tables(q)
         assert np.array_equal(qy, np.asarray(oy, np.uint8)) and np.array_equal(qc, np.asarray(oc, np.uint8)), q
+
+
+def test_huffman_array_emulation_matches_std_containers():
+    """huffman.cpp's per-frame builder (fixed arrays emulating libstdc++'s
+    unordered_map order and priority_queue heap) against the same algorithm on the
+    standard containers, which the tests above pin to the reference's Huffman.cpp."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "bin", "test_huffman_fast")
+    if not os.path.exists(exe):
+        pytest.skip("tests/cpp/bin/test_huffman_fast not built (make)")
+    r = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("0 mismatches")
