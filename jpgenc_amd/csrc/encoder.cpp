@@ -238,9 +238,6 @@ struct Encoder::Slot {
     uint32_t* d_tcount = nullptr;  // records per tile
     size_t cap_tiles = 0;          // (capacities: records, in words; tiles)
     size_t cap_recs = 0;
-    FusedTileInfo* d_tinfo = nullptr;  // fused K1: per K1 tile, the DC fix-up's inputs
-    size_t cap_tinfo = 0;
-    bool fused = false;            // this frame runs the fused K1 (+ DC fix-up) instead of K1 + K2
     uint8_t* d_out = nullptr;
     uint32_t* d_tab = nullptr;  // [1024] tables, then the header bytes (one upload)
     // pinned host staging
@@ -274,7 +271,7 @@ struct Encoder::Slot {
 
     ~Slot() {
         hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
-        hipFree(d_recs); hipFree(d_tcount); hipFree(d_tinfo);
+        hipFree(d_recs); hipFree(d_tcount);
         hipFree(d_out); hipFree(d_tab);
         hipHostFree(h_hist); hipHostFree(h_tab); hipHostFree(h_result);
         for (auto& e : ev) if (e) hipEventDestroy(e);
@@ -376,7 +373,6 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
     if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     if (const char* sw = std::getenv("JPGE_STATS_WGS")) e->stats_wgs_ = (uint32_t)std::strtoul(sw, nullptr, 10);
-    if (const char* fu = std::getenv("JPGE_FUSED")) e->fused_ = std::strtoul(fu, nullptr, 10) != 0;
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
@@ -471,21 +467,18 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         JPGE_HIP(hipMalloc((void**)&s.d_coef, nblk * 128));
         s.cap_blk = nblk;
     }
-    // (sized for the K2 layout and the fused one alike: a slot may run either)
-    const SegLayout fl = fused_layout(g, entropy_wgs());
-    const CtlLayout L(std::max(layout(g).grid(), fl.grid()));
-    const size_t ntiles = std::max<size_t>(seg_tiles(layout(g)), fused_tiles(g));
-    const size_t nrecs = std::max<size_t>((size_t)seg_tiles(layout(g)) * kTileRecords, (size_t)fused_tiles(g) * kFusedSlotRecs);
+    const CtlLayout L(layout(g).grid());
+    const size_t ntiles = seg_tiles(layout(g));
+    const size_t nrecs = (size_t)seg_tiles(layout(g)) * kTileRecords;
     if (ntiles > s.cap_tiles || nrecs > s.cap_recs) {
-        hipFree(s.d_recs); hipFree(s.d_tcount); hipFree(s.d_tinfo);
-        s.d_recs = nullptr; s.d_tcount = nullptr; s.d_tinfo = nullptr; s.cap_tiles = s.cap_recs = 0;
-        JPGE_HIP(hipMalloc((void**)&s.d_recs, nrecs * 4));
+        hipFree(s.d_recs); hipFree(s.d_tcount);
+        s.d_recs = nullptr; s.d_tcount = nullptr; s.cap_tiles = s.cap_recs = 0;
+        JPGE_HIP(hipMalloc((void**)&s.d_recs, nrecs * sizeof(*s.d_recs)));
         JPGE_HIP(hipMalloc((void**)&s.d_tcount, ntiles * 4));
-        JPGE_HIP(hipMalloc((void**)&s.d_tinfo, ntiles * sizeof(FusedTileInfo)));
         s.cap_tiles = ntiles;
         s.cap_recs = nrecs;
     }
-    const size_t ubuf = std::max(entropy_ubuf_bytes(layout(g)), entropy_ubuf_bytes(fl));
+    const size_t ubuf = entropy_ubuf_bytes(layout(g));
     if (ubuf > s.cap_ubuf) {
         hipFree(s.d_ubuf); s.d_ubuf = nullptr; s.cap_ubuf = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_ubuf, ubuf));
@@ -510,7 +503,7 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
 }
 
 SegLayout Encoder::slot_layout(const Slot& s) const {
-    return s.fused ? fused_layout(s.g, entropy_wgs()) : seg_layout(s.g, s.rst.mcus, entropy_wgs());
+    return seg_layout(s.g, s.rst.mcus, entropy_wgs());
 }
 
 // Kernel parameter blocks of a slot's frame (or stripe).
@@ -532,15 +525,6 @@ FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
     a.imp_src = imp ? reinterpret_cast<const uint4*>(imp->d_tab_host) : nullptr;
     a.imp_dst = imp ? reinterpret_cast<uint4*>(imp->d_tab) : nullptr;
     a.imp_n16 = imp ? (uint32_t)((kTabBytes + imp->hdr_len + 15) / 16) : 0u;
-    if (s.fused) {  // symbols instead of coefficients; the histograms are already zero
-        a.fused = true;
-        a.recs = s.d_recs;
-        a.tcount = s.d_tcount;
-        a.tinfo = s.d_tinfo;
-        a.hist.cnt = reinterpret_cast<uint32_t*>(s.d_ctl + L.cnt);
-        a.hist.key = reinterpret_cast<uint64_t*>(s.d_ctl + L.key);
-        a.zero_words = 0;
-    }
     a.dbg = d_dbg_;
     return a;
 }
@@ -589,8 +573,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     if (ext_place_ > 0 || (ext_place_ < 0 && lanes_.size() > 1)) {
         e.flags |= kExtPlace;
         // the last code workgroup places every workgroup (no placement launch); the
-        // counter is in the block K1 zeroes (the fused K1 does not zero it)
-        if (place_in_code_ && !s.fused && !s.rst.mcus && slot_layout(s).grid() <= kPlaceInCodeMaxWgs)
+        // counter is in the block K1 zeroes
+        if (place_in_code_ && !s.rst.mcus && slot_layout(s).grid() <= kPlaceInCodeMaxWgs)
             e.done = reinterpret_cast<uint32_t*>(s.d_ctl + L.done);
     }
     e.host_result = s.d_result_host;
@@ -601,7 +585,6 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.seed = s.seed;
     e.rst = s.rst;
     e.seg = slot_layout(s);
-    e.slot_words = s.fused ? (uint32_t)kFusedSlotRecs : 0u;
     if (s.rst.mcus) {  // a stripe's first interval follows the previous stripes' ones
         e.seg_index0 = s.rst.mcu0 / s.rst.mcus;
         e.seg_markers0 = e.seg_index0 > 0 ? 1u : 0u;
@@ -658,12 +641,6 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.key_y0 = s.key_c0 = s.key_ncb = 0;
     s.img_w = f.width;
     s.img_h = f.height;
-    // the fused K1 (symbols straight from the transform) for pipelined 4:2:0 frames
-    s.fused = fused_ && lanes_.size() > 1 && !s.rst.mcus && !g.row8() && g.bpm == 6 && !(flags & kFlagCoefficients);
-    if (s.fused) {  // (a fused K1 cannot zero them itself: its workgroups flush while others may not have started)
-        const CtlLayout Lc(slot_layout(s).grid());
-        JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, Lc.rec, s.stream));
-    }
     const FdctArgs a = fdct_args(s, f.maxval, imp);
     const StatsArgs st2 = stats_args(s);
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
@@ -672,18 +649,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
     const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
     JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
-    if (s.fused) {
-        FixupArgs fx;
-        fx.tinfo = s.d_tinfo;
-        fx.recs = s.d_recs;
-        fx.g = g;
-        fx.ntiles = fused_tiles(g);
-        fx.tiles_per_row = (g.mw + kFusedTileMcus - 1) / kFusedTileMcus;
-        fx.hist = a.hist;
-        JPGE_HIP(launch_dc_fixup(fx, s.stream, s.timed ? &t2 : nullptr));
-    } else {
-        JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2 : nullptr));
-    }
+    JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2 : nullptr));
     s.seq = ++seq_counter_;
     s.hist = st2.hist;
     if (export_hist)
@@ -1093,7 +1059,6 @@ int Encoder::stripe_transform(const StripeDesc& d, const uint8_t qy[64], const u
     s.rst = Restart();
     s.rst.mcus = restart_mcus_;
     s.rst.mcu0 = d.mcu_row0 * g.mw;
-    s.fused = false;
     s.key_y0 = 2ull * d.mcu_row0 * (2ull * g.mw);  // Y blocks above the stripe (raster)
     s.key_c0 = (uint64_t)d.mcu_row0 * g.mw;         // Cb blocks above it
     s.key_ncb = (uint64_t)mh_img * g.mw;            // Cb blocks of the image
@@ -1503,7 +1468,6 @@ int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_
     s.export_queued.store(0, std::memory_order_relaxed);
     // applyDCT(Arai) + applyQuantization (Image.cpp:844-871) into the MCU layout; the
     // control block is zeroed here (K1 does it on the RGB8 path)
-    s.fused = false;
     const CtlLayout L(layout(g).grid());
     JPGE_HIP(hipMemsetAsync(s.d_ctl, 0, L.total, st));
     PlaneBlockArgs b{};

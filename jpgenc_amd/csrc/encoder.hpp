@@ -22,7 +22,7 @@ namespace jpge {
 
 constexpr uint32_t kFlagDeviceInput = 1u;
 constexpr uint32_t kFlagDeviceOutput = 2u;
-constexpr uint32_t kFlagCoefficients = 1u << 30;  // (internal) the frame's coefficients are read back: no fused K1
+constexpr uint32_t kFlagCoefficients = 1u << 30;  // (internal) the frame's coefficients are read back
 
 struct FrameDesc {
     const uint8_t* rgb = nullptr;
@@ -151,7 +151,6 @@ class Encoder {
     std::unique_ptr<TablePool> pool_;
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
-    bool fused_ = false;        // JPGE_FUSED=1: the fused K1 (+ DC fix-up) for pipelined 4:2:0 frames (measured slower)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
     int mode_ = 420;            // subsampling mode (jpge_set_subsampling)
     // entropy workgroups: the override, else 512 for a single lane (its frames' latency:
@@ -162,7 +161,7 @@ class Encoder {
     // over 3 per CU; 1.5 per CU equal, 2.5 or 1 per CU slower)
     uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 0u : 512u); }
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
-    // the entropy partition a slot's current frame runs on (fused K1 frames: K1's tiles)
+    // the entropy partition a slot's current frame runs on
     SegLayout slot_layout(const Slot& s) const;
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch

@@ -47,7 +47,7 @@ constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
 constexpr int kMaxTiles = kEntropyMaxTilesPerWg;
-constexpr int kTcntSlots = kFusedTilesPerWg > kMaxTiles ? kFusedTilesPerWg : kMaxTiles;  // tiles of a workgroup, any layout
+constexpr int kTcntSlots = kMaxTiles;  // tiles of a workgroup
 constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-case tile + lead
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     // zeros), so no branch merges in-flight registers and the in-order wait for a
     // round's records never waits for the prefetch behind it.
     const uint32_t gt0 = wt.seg * a.seg.tps + wt.t0;  // global number of the first tile
-    const uint32_t slot = a.slot_words ? a.slot_words : (uint32_t)kTileRecords;  // record words per tile
+    constexpr uint32_t slot = kTileRecords;  // records per tile
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * slot), 0, ntl * slot * 4, 0x00020000);
     constexpr int kGroups = K3_GROUPS;            // groups of 4 records per thread and round
@@ -803,20 +803,6 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
     };
     part(L.sblk, L.tps, L.wps);
     part(L.lblk, L.ltps, L.lwps);
-    return L;
-}
-
-SegLayout fused_layout(const Geometry& g, uint32_t wgs_override) {
-    SegLayout L;
-    const uint32_t nt = fused_tiles(g);
-    const uint32_t want = wgs_override ? wgs_override : 384u;
-    const uint32_t lo = (nt + kFusedTilesPerWg - 1) / kFusedTilesPerWg;
-    // (a tile of one MCU codes >= 12 bits: every workgroup's stream has its 8 edge bits)
-    const uint32_t G = want < lo ? lo : (want > nt ? nt : want);
-    L.nseg = 1;
-    L.sblk = L.lblk = g.nblocks();
-    L.tps = L.ltps = nt;
-    L.wps = L.lwps = G;
     return L;
 }
 

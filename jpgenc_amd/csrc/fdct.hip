@@ -18,8 +18,6 @@
 // no contraction (-ffp-contract=off plus the pragma in device_common.hpp); the
 // colour conversion of 8-bit input uses FMA chains only where every partial result
 // is exact (all terms are multiples of 2^-27 far inside 53 bits).
-#include <type_traits>
-
 #include "arai.hpp"
 #include "device_common.hpp"
 
@@ -111,37 +109,12 @@ struct K1WaveLds {
 };
 constexpr int kQRow = 9;  // padded q-table rows: lanes reading rows j=0..7 hit distinct banks
 
-// Fused symbol pass (kernels.hpp FusedTileInfo): per wave, the tile's quantised rows
-// (cq, written by the rounds) and, once the rounds are done, the symbol steps'
-// scratch over the dead staging and transpose areas; per workgroup, histogram copies
-// and first-occurrence keys, as in K2 (stats.hip).
-constexpr int kFB = kFusedTileMcus * 6;  // blocks of a tile
-constexpr int kFHistCopies = 4;
-constexpr int kFCopyWords = 2 * 256 + 4, kFDcCopyWords = 2 * 16 + 4;
-struct K1SymScratch {
-    uint32_t nz[kFB * 63];  // the tile's AC non-zeros in stream order: v & 0xFFFF | p << 16 | blk << 22
-    uint64_t bmask[kFB];    // AC non-zero mask (bit p = zig-zag position p); bit 0: ZRL block
-    uint64_t lmask[kFB];    // ZRL block: the non-zeros after a run of 16+ zeros
-    uint2 binfo[kFB];       // x: AC key base (text index * 128, bit 31 Cr); y: (first record - first non-zero + 1) | chroma << 31
-    uint32_t nzbase[kFB];   // first non-zero of each block in nz
-    int dcv[kFB];           // DC of each block
-};
-static_assert(sizeof(K1SymScratch) <= sizeof(K1WaveLds), "the symbol scratch fits the staging area");
 template <int kWaves>
-struct K1FusedLds {
-    uint4 cq[kWaves][kFB * 8];  // the tile's quantised rows (8 int16), block-major in stream order
-    uint32_t acnt[kFHistCopies][kFCopyWords];
-    uint32_t dcnt[kFHistCopies][kFDcCopyWords];
-    uint32_t key[4][256];
-};
-struct K1NoFused {};
-template <int kWaves, bool kFused = false>
 struct K1Lds {
     K1WaveLds w[kWaves];
     uint32_t next;  // next tile of the workgroup's run to hand out
     double q[2][8 * kQRow];     // luma, chroma
     double invq[2][8 * kQRow];  // s_u / q (correctly rounded), u = column
-    std::conditional_t<kFused, K1FusedLds<kWaves>, K1NoFused> fx;
 };
 
 __device__ __forceinline__ double ycc_exact_y(uint32_t p) {
@@ -198,185 +171,10 @@ __device__ __forceinline__ void swap_halves(double& a, double& b) {
     b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
 }
 
-// The fused symbol pass over one tile (one wave; its quantised rows in cq, block
-// b = m * 6 + slot in stream order, nb = 6 x the tile's MCUs): the steps of K2
-// (stats.hip) on a wave's scale — masks and DCs, per-block counts and one DPP scan,
-// the non-zeros filed at their stream rank, then a lane per non-zero (run, ZRLs,
-// category, histogram, key, record) and a lane per block (DC difference, EOB).  The
-// first MCU's Y0 / Cb / Cr DCs predict from the previous tile: their records,
-// counts and keys are dc_fixup_kernel's; the tile info carries what it needs.
-// Text indices are relative to the workgroup's bases (ybase, cbase), as in K2.
-template <class Fx>
-__device__ __forceinline__ void fused_tile_symbols(const uint4* __restrict__ cq, K1SymScratch& S, Fx& fx, uint32_t* grec,
-                                                   uint32_t& ntot, FusedTileInfo* info, int nb, uint32_t mrow,
-                                                   uint32_t mcol0, uint32_t mw, uint32_t ybase, uint32_t cbase, int lane) {
-    // zig-zag positions of this lane's row (row = lane & 7 for every block row it holds)
-    uint32_t zlo = reinterpret_cast<const uint32_t*>(&kNatToZz[(lane & 7) * 8])[0];
-    uint32_t zhi = reinterpret_cast<const uint32_t*>(&kNatToZz[(lane & 7) * 8])[1];
-    asm volatile("" : "+v"(zlo), "+v"(zhi));  // (recomputed per tile, not held across the kernel)
-    constexpr int kRows = kFB * 8 / 64;
-    // ---- A: masks and DCs ----
-    uint4 rows[kRows];
-    uint64_t rowbits[kRows];
-#pragma unroll
-    for (int i = 0; i < kRows; ++i) {
-        const int q = lane + 64 * i, blk = q >> 3;
-        rows[i] = q < nb * 8 ? cq[q] : make_uint4(0, 0, 0, 0);
-        const uint32_t w[4] = {rows[i].x, rows[i].y, rows[i].z, rows[i].w};
-        uint64_t m = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
-            const uint32_t zp = ((u < 4 ? zlo : zhi) >> (8 * (u & 3))) & 0xFF;
-            m |= (uint64_t)(c != 0) << zp;
-        }
-        rowbits[i] = m & ~1ull;
-        m = or_lanes8(m);
-        if ((lane & 7) == 0 && blk < nb) {
-            S.bmask[blk] = m & ~1ull;
-            S.dcv[blk] = (int16_t)(w[0] & 0xFFFF);
-        }
-    }
-    wave_order();
-    // ---- B: one lane per block ----
-    const int b = lane;
-    const bool bact = b < nb;
-    const int m = b / 6, slot = b - 6 * (b / 6);
-    const int comp = slot < 4 ? 0 : slot - 3;
-    uint32_t cnt = 0, rel = 0;
-    uint64_t bm = 0;
-    if (bact) {
-        bm = S.bmask[b];
-        const uint32_t n = (uint32_t)__builtin_popcountll(bm);
-        const bool eob = !(bm >> 63);
-        const uint64_t x = bm | 1ull;
-        const int last = 63 - __builtin_clzll(x);
-        const uint64_t z = ~x & ((last ? (1ull << last) : 1ull) - 1ull);
-        uint64_t r = z & (z >> 1);
-        r &= r >> 2;
-        r &= r >> 4;
-        r &= r >> 8;
-        uint32_t zrl = 0;
-        if (r) {  // rare: the non-zeros after a run of 16+ zeros, and their ZRL count
-            const uint64_t L = bm & (r << 16);
-            for (uint64_t t = L; t; t &= t - 1) {
-                const int p = __builtin_ctzll(t);
-                zrl += (uint32_t)(p - (63 - __builtin_clzll(x & ((1ull << p) - 1ull))) - 1) >> 4;
-            }
-            bm |= 1ull;  // flag: a ZRL block
-            S.bmask[b] = bm;
-            S.lmask[b] = L;
-        }
-        cnt = (n << 16) | (1u + n + zrl + (eob ? 1u : 0u));
-        // the block's text index (Y: block raster order; all Cr after all Cb)
-        const uint32_t mcu = mrow * mw + mcol0 + (uint32_t)m;
-        if (comp == 0)
-            rel = (mrow * 2 + ((uint32_t)slot >> 1)) * (2 * mw) + (mcol0 + (uint32_t)m) * 2 + ((uint32_t)slot & 1) - ybase;
-        else
-            rel = (mcu - cbase) | (comp == 2 ? 0x80000000u : 0u);
-    }
-    const uint32_t incl = wave_scan_incl(cnt);
-    const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
-    const uint32_t ex = incl - cnt;
-    if (bact) {
-        S.nzbase[b] = ex >> 16;
-        S.binfo[b] = make_uint2((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7),
-                                ((ex & 0xFFFF) + 1 - (ex >> 16)) | (comp ? 0x80000000u : 0u));
-    }
-    wave_order();
-    // ---- C: the non-zeros at their stream rank ----
-#pragma unroll
-    for (int i = 0; i < kRows; ++i) {
-        if (!rowbits[i]) continue;
-        const int blk = (lane >> 3) + 8 * i;
-        const uint64_t bmk = S.bmask[blk] & ~1ull;
-        const uint32_t base = S.nzbase[blk];
-        const uint32_t w[4] = {rows[i].x, rows[i].y, rows[i].z, rows[i].w};
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int16_t c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
-            const uint32_t zp = ((u < 4 ? zlo : zhi) >> (8 * (u & 3))) & 0xFF;
-            if (zp != 0 && c != 0) {
-                const uint32_t rank = (uint32_t)__builtin_popcountll(bmk << (64u - zp));
-                S.nz[base + rank] = ((uint32_t)c & 0xFFFFu) | (zp << 16) | ((uint32_t)blk << 22);
-            }
-        }
-    }
-    wave_order();
-    // ---- D: a lane per non-zero ----
-    const uint32_t N = tot >> 16;
-    for (uint32_t e = (uint32_t)lane; e < N; e += 64) {
-        const uint32_t ent = S.nz[e];
-        const int v = (int16_t)(ent & 0xFFFF);
-        const int p = (int)((ent >> 16) & 63), blk = (int)(ent >> 22);
-        const uint64_t mk = S.bmask[blk];
-        int run = __builtin_clzll((mk | 1ull) << (64 - p));  // zeros since the previous non-zero
-        uint32_t zb = 0;  // ZRL records of this block up to and including this entry's
-        if (mk & 1ull) {
-            for (uint64_t t = S.lmask[blk] & (((1ull << p) - 1ull) | (1ull << p)); t; t &= t - 1) {
-                const int qq = __builtin_ctzll(t);
-                zb += (uint32_t)(qq - (63 - __builtin_clzll(mk & ((1ull << qq) - 1ull))) - 1) >> 4;
-            }
-        }
-        const int nzr = run >> 4;
-        run &= 15;
-        const int cat = category(v);
-        const int sym = (run << 4) | cat;
-        const uint2 bi = S.binfo[blk];
-        const int ts = (int)(bi.y >> 31);
-        atomicAdd(&fx.acnt[lane & (kFHistCopies - 1)][ts * 256 + sym], 1u);
-        const uint32_t kk = bi.x + 2u * p + 1u;
-        uint32_t* kp = &fx.key[2 * ts + 1][sym];
-        if (kk < *kp) atomicMin(kp, kk);
-        const uint32_t o = (bi.y & 0x7FFFFFFFu) + e + zb;  // recbase + 1 + rank + ZRLs
-        if (nzr) {  // its ZRLs (F/0) just before it
-            atomicAdd(&fx.acnt[lane & (kFHistCopies - 1)][ts * 256 + 0xF0], (uint32_t)nzr);
-            uint32_t* kz = &fx.key[2 * ts + 1][0xF0];
-            if (kk - 1u < *kz) atomicMin(kz, kk - 1u);
-            for (int zz = 1; zz <= nzr; ++zz) grec[o - zz] = rec_word(2 * ts + 1, 0xF0, 0);
-        }
-        grec[o] = rec_word(2 * ts + 1, (uint32_t)sym, extra_bits(v, cat));
-    }
-    // ---- a lane per block: DC difference (Image.cpp:638-678) and EOB ----
-    if (bact) {
-        const int tsel = comp != 0;
-        const uint32_t recb = ex & 0xFFFF;  // the block's first record
-        // the predecessor: the previous Y slot, 3 blocks back for an MCU's first Y
-        // block, 6 back for chroma; the first MCU's Y0 / Cb / Cr: dc_fixup_kernel
-        if (m > 0 || (slot >= 1 && slot <= 3)) {
-            const int back = (slot >= 1 && slot <= 3) ? 1 : (slot == 0 ? 3 : 6);
-            const int dd = S.dcv[b] - S.dcv[b - back];
-            const int dcat = category(dd);
-            atomicAdd(&fx.dcnt[lane & (kFHistCopies - 1)][tsel * 16 + dcat], 1u);
-            uint32_t* kp = &fx.key[2 * tsel][dcat];
-            if (rel < *kp) atomicMin(kp, rel);
-            grec[recb] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
-        }
-        if (!(bm >> 63)) {  // EOB: the block's last record
-            const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);
-            atomicAdd(&fx.acnt[lane & (kFHistCopies - 1)][tsel * 256], 1u);
-            uint32_t* ke = &fx.key[2 * tsel + 1][0];
-            if (acb + 127u < *ke) atomicMin(ke, acb + 127u);
-            grec[recb + (cnt & 0xFFFF) - 1] = rec_word(2 * tsel + 1, 0, 0);
-        }
-        if (b == 4) info->off_cb = (uint16_t)recb;
-        if (b == 5) info->off_cr = (uint16_t)recb;
-    }
-    ntot = tot & 0xFFFF;
-    const int lm = nb / 6 - 1;  // the tile's last MCU
-    if (lane < 6) {  // (lanes 4 and 5 wrote the offsets: other fields, other bytes)
-        const int src = lane < 3 ? (lane == 0 ? 0 : 3 + lane) : lm * 6 + lane;  // Y0 Cb Cr | Y3 Cb Cr
-        const int16_t dc = (int16_t)S.dcv[src];
-        if (lane < 3) info->dc_first[lane] = dc;
-        else info->dc_last[lane - 3] = dc;
-    }
-    wave_order();  // this tile's scratch reads before the next tile's staging
-}
-
-template <bool kExact, int kWaves, int kFilt, bool kFused = false>
+template <bool kExact, int kWaves, int kFilt>
 __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     constexpr int kK1Threads = kWaves * 64;
-    __shared__ K1Lds<kWaves, kFused> lds;
+    __shared__ K1Lds<kWaves> lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;  // wv: 0..15
     K1WaveLds& W = lds.w[wv];
     JPGE_STAMP(1);
@@ -444,15 +242,6 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
         lds.q[c][o] = q;
         lds.invq[c][o] = arai_scale(e & 7) / q;
     }
-    if constexpr (kFused) {
-        for (int i = tid; i < kFHistCopies * kFCopyWords; i += kK1Threads) (&lds.fx.acnt[0][0])[i] = 0;
-        for (int i = tid; i < kFHistCopies * kFDcCopyWords; i += kK1Threads) (&lds.fx.dcnt[0][0])[i] = 0;
-        for (int i = tid; i < 1024; i += kK1Threads) (&lds.fx.key[0][0])[i] = 0xFFFFFFFFu;
-    }
-    // key bases of the fused pass: Y raster index of the run's first MCU row's first Y
-    // row, chroma raster index of that MCU row (keys are relative to them, as in K2)
-    const uint32_t mrow0 = tb_p / tiles_per_row;
-    const uint32_t ybase = mrow0 * 4 * mw, cbase = mrow0 * mw;
     // LDS-only barrier: the prologue's shared state is in LDS (a full __syncthreads
     // would also wait for the first tile's pixels, issued above)
     lds_barrier();
@@ -625,10 +414,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
             arai8_unscaled(x, o);  // y(j, u) = o[u] * s_u
             pk = quant_row(o, iqc, &lds.q[qb][j * kQRow]);
             const uint32_t blk = (mrow * mw + mcol0 + m) * 6 + slot;
-            off = (!kFused && m < nvalid) ? blk * 128 + j * 16 : kOob;
-            if constexpr (kFused) {  // the row to the tile's LDS copy (no coefficient store)
-                if (m < nvalid) lds.fx.cq[wv][(m * 6 + slot) * 8 + j] = make_uint4(pk.x, pk.y, pk.z, pk.w);
-            }
+            off = m < nvalid ? blk * 128 + j * 16 : kOob;
         };
         {
             double x[8];
@@ -655,41 +441,12 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
             finish(x, 2 + (b8 >> 2), b8 & 3, 0, pend, poff, [] {});
         }
         wave_order();  // the next tile's staging overwrites the transpose buffer
-        if constexpr (kFused) {
-            uint32_t ntot;
-            fused_tile_symbols(lds.fx.cq[wv], reinterpret_cast<K1SymScratch&>(W), lds.fx,
-                               a.recs + (uint64_t)t * kFusedSlotRecs, ntot, a.tinfo + t, nvalid * 6, mrow, mcol0,
-                               mw, ybase, cbase, lane);
-            if (lane == 0) a.tcount[t] = ntot;
-        }
         k = kn;
         kn = kn2;
     }
     store_pending();
     __syncthreads();
     JPGE_STAMP(7);
-    if constexpr (kFused) {  // the workgroup's counts and keys into the frame's replicas (as K2's flush)
-        const int rep = blockIdx.x % kHistReplicas;
-        const uint64_t ncb = a.g.nmcu();  // Cb blocks of the image (every Cr key follows them)
-        for (int i = tid; i < 1024; i += kK1Threads) {
-            const int t = i >> 8, sy = i & 255;
-            const bool ac = t & 1;
-            uint32_t c = 0;
-            if (ac) {
-                for (int cp = 0; cp < kFHistCopies; ++cp) c += lds.fx.acnt[cp][(t >> 1) * 256 + sy];
-            } else if (sy < 16) {
-                for (int cp = 0; cp < kFHistCopies; ++cp) c += lds.fx.dcnt[cp][(t >> 1) * 16 + sy];
-            }
-            if (!c) continue;
-            atomicAdd(&a.hist.cnt[(rep * 4 + t) * 256 + sy], c);
-            const uint32_t k32 = lds.fx.key[t][sy];
-            const uint64_t base = t < 2 ? (uint64_t)ybase : (uint64_t)cbase + ((k32 & 0x80000000u) ? ncb : 0ull);
-            const uint64_t gkey = (ac ? base * 128ull : base) + (k32 & 0x7FFFFFFFu);
-            const unsigned long long inv = ~gkey;
-            unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[t * 256 + sy]);
-            if (inv > *gk) atomicMax(gk, inv);
-        }
-    }
 }
 
 // ---- MCUs one block row high: 4:4:4, 4:2:2, 4:1:1 (applySubsampling S444, S422,
@@ -902,9 +659,6 @@ void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t
     if (a.solo) {
         if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
         else (void)launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
-    } else if (a.fused) {
-        if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt, true>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
-        else (void)launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt, true>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
     } else {
         if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
         else (void)launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);

@@ -66,7 +66,6 @@ struct HistPtrs {
     uint64_t* key;
 };
 
-struct FusedTileInfo;
 struct FdctArgs {
     const uint8_t* rgb;
     uint64_t stride;
@@ -84,36 +83,7 @@ struct FdctArgs {
     const uint4* imp_src;
     uint4* imp_dst;
     uint32_t imp_n16;
-    // fused symbol pass (4:2:0, whole frames, the shared shape; fused = false: off):
-    // the tile's symbol records instead of its coefficients (see FusedTileInfo)
-    bool fused = false;
-    uint32_t* recs = nullptr;       // [K1 tiles][kFusedSlotRecs]
-    uint32_t* tcount = nullptr;     // [K1 tiles] records per tile
-    FusedTileInfo* tinfo = nullptr;  // [K1 tiles] the DC fix-up's inputs
-    HistPtrs hist{};                // the frame's histogram replicas and keys
     uint64_t* dbg;   // diagnostic phase stamps (JPGE_STAMPS builds), else unused
-};
-
-// Fused K1 (4:2:0 pipeline frames): each K1 tile (4 MCUs of one MCU row, 24 blocks)
-// codes its own symbols into a slot of kFusedSlotRecs records.  The DC of the tile's
-// first MCU (Y0, Cb, Cr) predicts from the previous tile, which another wave codes:
-// those three DC records are left to dc_fixup_kernel, which reads each tile's info.
-constexpr int kFusedTileMcus = 4;
-constexpr int kFusedSlotRecs = kFusedTileMcus * 6 * 64;
-constexpr int kFusedTilesPerWg = 21;  // entropy workgroup: <= 21 x 24 blocks (the region holds 512)
-struct FusedTileInfo {
-    int16_t dc_first[3];  // DC of the first MCU's Y0, Cb, Cr
-    int16_t dc_last[3];   // DC of the last MCU's Y3 (last Y slot), Cb, Cr
-    uint16_t off_cb, off_cr;  // record offsets of the first MCU's Cb and Cr DC (Y0's is 0)
-};
-static_assert(sizeof(FusedTileInfo) == 16, "tile info size");
-
-struct FixupArgs {
-    const FusedTileInfo* tinfo;
-    uint32_t* recs;
-    Geometry g;
-    uint32_t ntiles, tiles_per_row;
-    HistPtrs hist;
 };
 
 // Stripe context of a frame (a row stripe of a larger image); the
@@ -260,7 +230,6 @@ struct EntropyArgs {
     StripeSummary* summary = nullptr;  // summary mode output
     Restart rst;                       // restart intervals (rst.mcus = 0: none)
     SegLayout seg;                     // workgroup partition (host: seg_layout)
-    uint32_t slot_words = 0;           // record words per tile slot (0: kTileRecords; fused K1: kFusedSlotRecs)
     uint32_t seg_markers0 = 0;         // RST markers in this output before the frame's first segment (stripes)
     uint32_t seg_index0 = 0;           // the image's interval index of the frame's first segment (stripes)
     uint64_t out_base = 0;             // restart stripes: bytes of earlier stripes after the header
@@ -302,16 +271,12 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs = 0);
 // entropy partition of a frame: restart_mcus = 0 -> one segment over 128-block tiles
 // (2..kEntropyMaxTilesPerWg per workgroup, about 384 workgroups or wgs_override)
 SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_override);
-// fused K1 frames: one segment whose tiles are K1's (4 MCUs of a row), <= kFusedTilesPerWg per workgroup
-SegLayout fused_layout(const Geometry& g, uint32_t wgs_override);
-inline uint32_t fused_tiles(const Geometry& g) { return ((g.mw + kFusedTileMcus - 1) / kFusedTileMcus) * g.mh; }
 inline uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) { return seg_layout(g, 0, wgs_override).grid(); }
 
 inline uint64_t entropy_ubuf_bytes(const SegLayout& L) { return (uint64_t)L.grid() * kEntropyRegionBytes; }
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t = nullptr);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t = nullptr);
-hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s, const KTimer* t = nullptr);
 // [4][256] summed counts and keys into (mapped) host memory, then *host_seq = seq
 hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
                               uint64_t seq, hipStream_t s);

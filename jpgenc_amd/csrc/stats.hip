@@ -389,62 +389,6 @@ __global__ __launch_bounds__(1024) void hist_export_kernel(HistPtrs h, uint32_t*
     export_hist<1024>(h, host_cnt, host_key, host_seq, seq, threadIdx.x);
 }
 
-// DC fix-up of fused K1 frames (kernels.hpp FusedTileInfo): the first MCU of every
-// K1 tile predicts its Y0 / Cb / Cr DC from the previous tile's last MCU (Y3, Cb, Cr;
-// the frame's first MCU from 0), which another wave coded.  One thread per tile
-// writes the three DC records at their offsets in the tile's slot and counts their
-// categories and first-occurrence keys (workgroup LDS, then the frame's replicas).
-constexpr int kFixThreads = 256;
-__global__ __launch_bounds__(kFixThreads) void dc_fixup_kernel(FixupArgs a) {
-    __shared__ uint32_t cnt[2][16];
-    __shared__ unsigned long long key[2][16];  // minimum global key (text index)
-    const int tid = threadIdx.x;
-    if (tid < 32) {
-        cnt[tid >> 4][tid & 15] = 0;
-        key[tid >> 4][tid & 15] = ~0ull;
-    }
-    __syncthreads();
-    const uint32_t t = blockIdx.x * kFixThreads + tid;
-    if (t < a.ntiles) {
-        const FusedTileInfo f = a.tinfo[t];
-        int pred[3] = {0, 0, 0};
-        if (t > 0) {
-            const FusedTileInfo p = a.tinfo[t - 1];
-            pred[0] = p.dc_last[0];
-            pred[1] = p.dc_last[1];
-            pred[2] = p.dc_last[2];
-        }
-        const uint32_t mw = a.g.mw, mrow = t / a.tiles_per_row, mcol0 = (t % a.tiles_per_row) * kFusedTileMcus;
-        const uint64_t mcu = (uint64_t)mrow * mw + mcol0;
-        uint32_t* grec = a.recs + (uint64_t)t * kFusedSlotRecs;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const int dd = f.dc_first[c] - pred[c];
-            const int dcat = category(dd);
-            const int tsel = c != 0;
-            const uint32_t off = c == 0 ? 0u : (c == 1 ? f.off_cb : f.off_cr);
-            grec[off] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
-            atomicAdd(&cnt[tsel][dcat], 1u);
-            // text index: Y0 of the MCU in Y raster order; Cb the MCU; Cr after all Cb
-            const uint64_t k = c == 0 ? (uint64_t)mrow * 4 * mw + (uint64_t)mcol0 * 2
-                                      : mcu + (c == 2 ? (uint64_t)a.g.nmcu() : 0ull);
-            atomicMin(&key[tsel][dcat], (unsigned long long)k);
-        }
-    }
-    __syncthreads();
-    if (tid < 32) {
-        const int tsel = tid >> 4, s = tid & 15;
-        const uint32_t c = cnt[tsel][s];
-        if (c) {
-            const int rep = blockIdx.x % kHistReplicas;
-            atomicAdd(&a.hist.cnt[(rep * 4 + 2 * tsel) * 256 + s], c);
-            const unsigned long long inv = ~key[tsel][s];
-            unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[(2 * tsel) * 256 + s]);
-            if (inv > *gk) atomicMax(gk, inv);
-        }
-    }
-}
-
 }  // namespace
 
 hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
@@ -461,11 +405,6 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     const uint32_t g = tiles < want ? tiles : want;
     const uint32_t need = (tiles + kK2MaxRun - 1) / kK2MaxRun;
     return g > need ? g : need;
-}
-
-hipError_t launch_dc_fixup(const FixupArgs& a, hipStream_t s, const KTimer* t) {
-    if (!a.ntiles) return hipSuccess;
-    return launch_timed(t, dc_fixup_kernel, dim3((a.ntiles + kFixThreads - 1) / kFixThreads), dim3(kFixThreads), s, a);
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {

@@ -263,15 +263,13 @@ def test_encode_files_reports_bad_file(encoder, tmp_path):
         assert f.read() == _oracle.encode(J.synth_rgb8(1, 32, 32), 50)
 
 
-# The fused K1 path (JPGE_FUSED=1; kernels.hpp FusedTileInfo): symbols coded inside
-# the transform kernel per 4-MCU tile, the first MCU's DCs fixed up from the previous
-# tile, the entropy kernels over K1's tiles.  Ragged widths leave a last tile of 1-3
-# MCUs per row; single-MCU frames have one tile.
+# Single frames and batches over the lanes (each frame its own tables) at ragged
+# sizes and entropy partitions: one workgroup, 7, and the default.
 @pytest.mark.parametrize("wgs", [0, 1, 7])
 @pytest.mark.parametrize("w,h,kind,quality", [(1, 1, 0, 90), (16, 16, 1, 100), (37, 23, 0, 50), (200, 136, 2, 90),
                                               (500, 300, 1, 95), (1040, 48, 0, 75), (1920, 1080, 0, 90)])
-def test_fused_k1_bit_exact(wgs, w, h, kind, quality):
-    enc = _encoder_with_env(JPGE_FUSED=1, JPGE_ENTROPY_WGS=wgs)
+def test_pipeline_shapes_bit_exact(wgs, w, h, kind, quality):
+    enc = _encoder_with_env(JPGE_ENTROPY_WGS=wgs)
     try:
         rgb = J.synth_rgb8(77 + kind + w, w, h, kind=kind)
         assert enc.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
