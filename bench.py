@@ -758,19 +758,17 @@ def run_frames(args, rank, local, world, pg):
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H) if args.subsampling == 420 else {}
     yh, yv = J.SUBSAMPLING[args.subsampling]
     cb = 2.0 * 64 * (yh * yv + 2) / (64 * yh * yv)  # int16 coefficient bytes per pixel (4:2:0: 3)
-    # symbol records (2 B each, one per Huffman-coded symbol; the raw records of the rare
-    # symbols with more extra bits than a record holds, 0.06% at 4K Q90, are not counted):
-    # written by K2, read by K3
-    rec_bytes = 2.0 * tm["symbols"] / max(1, tm["frames"])
+    # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3
+    rec_bytes = 4.0 * tm["symbols"] / max(1, tm["frames"])
     # per-kernel algorithmic bytes per launch; the entropy stage is two
     # kernels: code (records -> the unstuffed bit stream) and pack (-> stuffed .jpg)
     alg = {
         "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
-        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 2 B each"),
-        "entropy_code_kernel": (rec_bytes + avg_jpeg, "symbol records read 2 B each + bit stream written (~.jpg size)"),
+        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 4 B each"),
+        "entropy_code_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + bit stream written (~.jpg size)"),
         "entropy_pack_kernel": (2.0 * avg_jpeg, "bit stream read + stuffed .jpg bytes written"),
     }
-    stage_alg = {"entropy_stage": (rec_bytes + avg_jpeg, "symbol records read 2 B each + .jpg bytes written")}
+    stage_alg = {"entropy_stage": (rec_bytes + avg_jpeg, "symbol records read 4 B each + .jpg bytes written")}
     tm_key = {"fdct_kernel": "fdct_sum", "stats_kernel": "dc_stats_sum", "entropy_code_kernel": "code_sum",
               "entropy_pack_kernel": "pack_sum", "entropy_stage": "entropy_sum"}
     pmc_key = {"entropy_stage": "entropy_kernel"}

@@ -65,7 +65,7 @@ typedef struct {
     float total;    /* K1 start .. K3 end of that frame (includes the queued work of other frames) */
     double fdct_sum, dc_stats_sum, entropy_sum; /* accumulated since jpge_reset_timing (ms) */
     uint64_t frames;                            /* frames accumulated */
-    uint64_t symbols; /* Huffman-coded symbols of those frames (K2's 16-bit records, less the rare raw ones) */
+    uint64_t symbols; /* Huffman-coded symbols of those frames (= K2's 4-byte symbol records) */
     double code_sum, pack_sum; /* K3's entropy_code_kernel and entropy_pack_kernel alone (ms, accumulated) */
 } jpge_timing;
 

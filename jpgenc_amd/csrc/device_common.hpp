@@ -85,11 +85,10 @@ __device__ __forceinline__ int category(int v) {
     return av ? 32 - __builtin_clz((unsigned)av) : 0;
 }
 
-// 16-bit symbol records (kernels.hpp): an AC record holds the top min(cat, 6) extra
-// bits, a DC record the top min(cat, 10); the rest go to a raw record after it.
-__device__ __forceinline__ uint32_t ac_rec(uint32_t t, uint32_t sym, uint32_t e6) { return (t << 14) | (sym << 6) | e6; }
-__device__ __forceinline__ uint32_t dc_rec(uint32_t t, uint32_t cat, uint32_t e10) { return (t << 14) | (cat << 10) | e10; }
-__device__ __forceinline__ uint32_t raw_rec(uint32_t n, uint32_t e) { return kRawRec | (n << 6) | e; }
+// Symbol record words (kernels.hpp): table << 24 | symbol << 16 | extra bits.
+__device__ __forceinline__ uint32_t rec_word(uint32_t table, uint32_t sym, uint32_t bits) {
+    return (table << 24) | (sym << 16) | bits;
+}
 __device__ __forceinline__ uint32_t extra_bits(int v, int cat) {  // getCategoryAndCode, Coding.hpp:214-221
     return (uint32_t)(v + (v >> 31)) & ((1u << cat) - 1);
 }

@@ -85,27 +85,14 @@ __device__ __forceinline__ uint32_t byte_range(int lo, int hi) {
     return ge & lt & 0x80808080u;
 }
 
-// One 16-bit symbol record (K2, kernels.hpp) as code bits: the table entry at r >> 6
-// (the record's table and symbol, and for DC records the top 4 of its 10 extra-bit
-// positions; see rec_table) gives the code, its length and how many of the record's
-// low bits are extra bits; returns the bit count (<= 16 + 10).
+// One symbol record (K2, kernels.hpp) as code bits: the table's code, then the
+// extra bits (the category's count of them); returns the bit count (<= 16 + 15).
 __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, uint32_t& bits) {
-    const uint32_t ent = tab[r >> 6];
-    const uint32_t ne = ent >> 24;
-    bits = ((ent & 0xFFFF) << ne) | (r & ((1u << ne) - 1u));
-    return ((ent >> 16) & 0xFF) + ne;
-}
-// Entry i of the decode table from the frame's code tables ([4][256] (len << 16) | code):
-// AC (t odd): symbol i & 255, its code and min(size, 6) extra bits in the record;
-// DC (t even): category (i >> 4) & 15 for all 16 values of the index's low nibble (the
-// top 4 extra-bit positions), min(cat, 10) extra bits; category 15: a raw record of
-// (i & 15) bits and no code.
-__device__ __forceinline__ uint32_t rec_table(const uint32_t* tables, uint32_t i) {
-    const uint32_t t = i >> 8, lo = i & 255;
-    if (t & 1) return tables[i] | (min(lo & 15u, 6u) << 24);
-    const uint32_t c = lo >> 4;
-    if (c == 15) return (lo & 15u) << 24;
-    return tables[(t << 8) | c] | (min(c, 10u) << 24);
+    const uint32_t sym = (r >> 16) & 0xFF, t = r >> 24;
+    const uint32_t nb = (t & 1) ? (sym & 15) : sym;  // AC: the symbol's size; DC: its category
+    const uint32_t ent = tab[(t << 8) | sym];
+    bits = ((ent & 0xFFFF) << nb) | (r & 0xFFFF);
+    return (ent >> 16) + nb;
 }
 
 // every workgroup's WgPlace from the records (the placement scan), kK3Threads threads
@@ -121,7 +108,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         export_hist<kK3Threads>(a.exp_hist, a.exp_cnt, a.exp_key, a.exp_seq, a.exp_seqv, tid);
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
-    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = rec_table(a.tables, (uint32_t)i);
+    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
     for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
     const int ntl = (int)wt.nt;
@@ -156,7 +143,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     const uint32_t gt0 = wt.seg * a.seg.tps + wt.t0;  // global number of the first tile
     constexpr uint32_t slot = kTileRecords;  // records per tile
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(a.recs + (uint64_t)gt0 * slot), 0, ntl * slot * 2, 0x00020000);
+        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * slot), 0, ntl * slot * 4, 0x00020000);
     constexpr int kGroups = K3_GROUPS;            // groups of 4 records per thread and round
     constexpr uint32_t kRound = 4 * kGroups * kK3Threads;  // records per round
     // The workgroup's records are one stream over its tiles: tile t's count padded to a
@@ -169,7 +156,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     total = __builtin_amdgcn_readfirstlane(total);
     uint32_t cs = 0, cpre = 0;  // this thread's tile cursor (tile, its first padded index)
     // the thread's 4 records from stream index i (nvalid: how many are records)
-    auto rec_load = [&](uint32_t i, uint32_t& nvalid) -> uint2 {
+    auto rec_load = [&](uint32_t i, uint32_t& nvalid) -> uint4 {
         while (cs < (uint32_t)ntl) {
             const uint32_t n = (L.tcnt[cs] + 3u) & ~3u;
             if (i < cpre + n) break;
@@ -181,15 +168,14 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         if (cs < (uint32_t)ntl) {
             const uint32_t rel = i - cpre, c = L.tcnt[cs];
             nvalid = c > rel ? min(c - rel, 4u) : 0u;
-            off = (cs * slot + rel) * 2;
+            off = (cs * slot + rel) * 4;
         }
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rec_rs, off, 0, 0);  // 4 records
-        return make_uint2(v[0], v[1]);
+        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rec_rs, off, 0, 0));
     };
     constexpr uint32_t kStageBits = (kStageWords - 2) * 32;
-    constexpr uint32_t kRoundMaxBits = kRound * 26;  // (a record codes at most 16 + 10 bits)
+    constexpr uint32_t kRoundMaxBits = kRound * 27;  // (a record codes at most 16 + 11 bits)
     static_assert(kStageBits > kRoundMaxBits, "the stage holds a round");
-    uint2 nxt[kGroups];
+    uint4 nxt[kGroups];
     uint32_t nvn[kGroups];
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) nxt[g] = rec_load(4 * (kGroups * tid + g), nvn[g]);
@@ -200,10 +186,10 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
 
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
-            const uint2 rv = nxt[g];
+            const uint4 rv = nxt[g];
             const uint32_t nv = nvn[g];
             nxt[g] = rec_load(r0 + kRound + 4 * (kGroups * tid + g), nvn[g]);  // the next round's (prefetch)
-            const uint32_t rr[4] = {rv.x & 0xFFFF, rv.x >> 16, rv.y & 0xFFFF, rv.y >> 16};
+            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
             gl[g] = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {

@@ -143,21 +143,15 @@ JPGE_HD inline WgTiles wg_tiles(const SegLayout& L, uint32_t w) {
 }
 
 // Symbol records (K2 -> K3): the entropy-coded symbols of a tile in stream order,
-// 16 bits each.  t = table (0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC):
-//   AC (t odd)   t << 14 | symbol << 6 | e6    e6: the top min(cat, 6) extra bits (cat = symbol & 15)
-//   DC (t even)  t << 14 | cat << 10 | e10     e10: the top min(cat, 10) extra bits
-//   raw          15 << 10 | n << 6 | e         the remaining n (<= 6) extra bits of the record before it
-// (a DC category field of 15 never occurs: DC categories are <= 12).  A symbol with more
-// extra bits than its record holds (AC cat >= 7, |v| >= 64: 0.06% of 4K Q90 symbols;
-// DC cat >= 11) is followed by one raw record.  The entropy kernel turns any record into
-// code bits from one table entry indexed by record >> 6 (entropy.hip rec_bits).
-// A block codes at most 128 records (a DC and its raw record, 63 AC symbols with theirs),
-// so a tile's records fit kTileRecords; tile t's sit at recs + t * kTileRecords, its
-// count at tcount[t].  Tiles are the entropy partition's (seg_layout), numbered
+// one u32 each: table << 24 | symbol << 16 | extra bits (table 0 Y-DC, 1 Y-AC,
+// 2 C-DC, 3 C-AC; the extra bits' count is the symbol's category: symbol & 15 for
+// AC, the symbol itself for DC).  A block codes at most 64 symbols (DC + 63 AC, or
+// DC + 62 AC + EOB; a zero run long enough for a ZRL removes a coefficient), so a
+// tile's records fit kTileRecords words; tile t's sit at recs + t * kTileRecords,
+// its count at tcount[t].  Tiles are the entropy partition's (seg_layout), numbered
 // segment by segment.
-constexpr int kRecPerBlock = 128;
+constexpr int kRecPerBlock = 64;
 constexpr int kTileRecords = kEntropyTile * kRecPerBlock;
-constexpr uint32_t kRawRec = 15u << 10;
 
 struct StatsArgs {
     const int16_t* coef;
@@ -170,7 +164,7 @@ struct StatsArgs {
     // Cb block, and the image's Cb block count (every Cr key follows all Cb keys)
     uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
     SegLayout seg;       // the entropy partition: the tiles the records are written in
-    uint16_t* recs;      // [tiles][kTileRecords] symbol records
+    uint32_t* recs;      // [tiles][kTileRecords] symbol records
     uint32_t* tcount;    // [tiles] records per tile
     uint32_t wgs = 0;    // workgroup count (0 = 3 per CU; the pipeline passes its own, stats_grid)
     uint64_t* dbg;
@@ -204,7 +198,7 @@ constexpr uint32_t kExtPlace = 4u;     // pack kernel reads WgPlace (entropy_sca
 
 struct EntropyArgs {
     const int16_t* coef;
-    const uint16_t* recs;    // the statistics kernel's symbol records (kTileRecords per tile)
+    const uint32_t* recs;    // the statistics kernel's symbol records (kTileRecords per tile)
     const uint32_t* tcount;  // records per tile
     Geometry g;
     const uint32_t* tables;  // [4][256] (len << 16) | code, followed by the header bytes

@@ -65,48 +65,16 @@ __device__ __forceinline__ uint32_t udiv24(uint32_t x, uint32_t d, float inv, ui
     return q;
 }
 
-// 0xFFC0 in each 16-bit half where |coefficient| >= 64 (an AC value with >= 7 extra
-// bits; row0: the row's first half is the DC, excluded)
-__device__ __forceinline__ uint32_t big_halves(const uint4& v, bool row0) {
-    typedef short s16x2 __attribute__((ext_vector_type(2)));
-    auto mag = [](uint32_t w) {
-        const s16x2 h = __builtin_bit_cast(s16x2, w);
-        return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, (s16x2)(0) - h));
-    };
-    return (mag(row0 ? v.x & 0xFFFF0000u : v.x) | mag(v.y) | mag(v.z) | mag(v.w)) & 0xFFC0FFC0u;
-}
-
-// A special block's (ZRL or big coefficients) records before entry p, and whether the
-// entry at p is big: ZRL records of the long runs at or before p (a ZRL comes before
-// its coefficient), raw records of the big coefficients before p.
-__device__ __forceinline__ uint32_t special_before(uint64_t m, uint64_t big, int p, bool& isbig) {
-    const uint64_t x = m | 1ull;
-    const int last = 63 - __builtin_clzll(x);
-    const uint64_t z = ~x & ((last ? (1ull << last) : 1ull) - 1ull);
-    uint64_t r = z & (z >> 1);
-    r &= r >> 2;
-    r &= r >> 4;
-    r &= r >> 8;
-    uint32_t zb = 0;
-    for (uint64_t t = m & (r << 16) & (((1ull << p) - 1ull) | (1ull << p)); t; t &= t - 1) {
-        const int q = __builtin_ctzll(t);
-        zb += (uint32_t)(q - (63 - __builtin_clzll(x & ((1ull << q) - 1ull))) - 1) >> 4;
-    }
-    isbig = (big >> p) & 1ull;
-    return zb + (uint32_t)__builtin_popcountll(big & ((1ull << p) - 1ull));
-}
-
 struct K2Lds {
     uint32_t nz[kMaxNz];                 // the tile's AC non-zeros in stream order: v & 0xFFFF | p << 16 | blk << 22
     uint32_t acnt[kHistCopies][kCopyWords];  // AC counters (Y-AC at 0, C-AC at 256), per copy
     uint32_t dcnt[kHistCopies][kDcCopyWords];  // DC counters (Y-DC at 0, C-DC at 16), per copy
     uint32_t key[4][256];                // workgroup-relative first-occurrence key (min)
-    uint64_t bmask[kK2Blocks];           // AC non-zero mask (bit p = zig-zag position p); bit 0: special block
-    uint64_t bigm[kK2Blocks];            // AC coefficients with >= 7 extra bits (|v| >= 64: a raw record each)
+    uint64_t bmask[kK2Blocks];           // AC non-zero mask (bit p = zig-zag position p); bit 0: ZRL block
+    uint64_t lmask[kK2Blocks];           // ZRL block: the non-zeros after a run of 16+ zeros
     uint32_t nzbase[kK2Blocks];          // first non-zero of each block in nz
     // per block, read together by the symbol step: x = AC key base (text index * 128,
-    // bit 31: Cr), y = (first record - first non-zero + 1 + dbig) | dbig << 30 | chroma << 31
-    // (dbig: the DC difference takes a raw record after its own)
+    // bit 31: Cr), y = (first record - first non-zero + 1) | chroma << 31
     uint2 binfo[kK2Blocks];
     int dcv[kK2Blocks];                  // DC of each block
     int prevdc[6];
@@ -176,7 +144,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
         const uint32_t ti = tile - t_first;
         const uint64_t tb = lds.tb0[ti];
         const int tnb = (int)(lds.tb0[ti + 1] - lds.tb0[ti]);
-        uint16_t* grec = a.recs + (uint64_t)tile * kTileRecords;
+        uint32_t* grec = a.recs + (uint64_t)tile * kTileRecords;
         uint32_t rec0 = 0;  // the tile's records before this step
       for (int s0 = 0; s0 < tnb; s0 += kK2Blocks) {
         const uint64_t b0 = tb + (uint64_t)s0;
@@ -187,7 +155,6 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
         // positions and 8 64-bit masks derived from them live across the whole loop)
         asm volatile("" : "+v"(regs.zlo), "+v"(regs.zhi));
         uint64_t rowbits[kPer];  // zig-zag positions of this lane's non-zero AC values
-        uint32_t rowbig = 0;     // this lane's rows hold an AC value with |v| >= 64
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const int q = tid + i * kK2Threads;
@@ -201,7 +168,6 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                 const uint32_t zp = ((u < 4 ? regs.zlo : regs.zhi) >> (8 * (u & 3))) & 0xFF;
                 m |= (uint64_t)(c != 0) << zp;  // (rows past the tile were loaded as zeros)
             }
-            rowbig |= big_halves(regs.v[i], row == 0);
             rowbits[i] = m & ~1ull;
             m = or_lanes8(m);  // the block's 8 rows
             if (ok && row == 0) {
@@ -209,45 +175,19 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                 lds.dcv[blk] = (int16_t)(w[0] & 0xFFFF);
             }
         }
-        // blocks' big-coefficient masks (their raw records; rare at Q90: a wave that
-        // holds none writes zeros)
-        if (__builtin_amdgcn_ballot_w64(rowbig != 0)) {
-#pragma unroll
-            for (int i = 0; i < kPer; ++i) {
-                const int q = tid + i * kK2Threads;
-                const int blk = q >> 3, row = q & 7;
-                const uint32_t w[4] = {regs.v[i].x, regs.v[i].y, regs.v[i].z, regs.v[i].w};
-                uint64_t g = 0;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int c = (int16_t)(u & 1 ? w[u >> 1] >> 16 : w[u >> 1] & 0xFFFF);
-                    const uint32_t zp = ((u < 4 ? regs.zlo : regs.zhi) >> (8 * (u & 3))) & 0xFF;
-                    g |= (uint64_t)(c >= 64 || c <= -64) << zp;
-                }
-                g = or_lanes8((uint64_t)(g & ~(uint64_t)1));
-                if (q < nb * 8 && row == 0) lds.bigm[blk] = g;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < kPer; ++i) {
-                const int q = tid + i * kK2Threads;
-                if (q < nb * 8 && (q & 7) == 0) lds.bigm[q >> 3] = 0;
-            }
-        }
         if (tid < 6) lds.prevdc[tid] = regs.prev_dc;
         lds_barrier();
         JPGE_ACC(0, tq);
-        // ---- B: per block counts, ZRL test, DC difference, key index; one scan ----
+        // ---- B: per block counts, ZRL test, key index; one scan ----
         uint32_t cnt = 0;
         const int b = tid;
         const bool bact = b < nb;
         int comp = 0;
         uint32_t rel = 0;  // the block's text index (relative to the key bases; bit 31: Cr)
-        int dd = 0;        // its DC difference to the chain predecessor (Image.cpp:638-678)
-        uint32_t dbig = 0; // the difference takes a raw record (DC category > 10)
+        int k = 0;         // its slot in its MCU
+        uint32_t m6 = 0;   // its MCU
         if (bact) {
             uint64_t m = lds.bmask[b];
-            const uint64_t big = lds.bigm[b];
             const uint32_t n = (uint32_t)__builtin_popcountll(m);
             const bool eob = !(m >> 63);
             const uint64_t x = m | 1ull;
@@ -265,13 +205,15 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
                     const int p = __builtin_ctzll(t);
                     zrl += (uint32_t)(p - (63 - __builtin_clzll(x & ((1ull << p) - 1ull))) - 1) >> 4;
                 }
+                lds.bmask[b] = m | 1ull;  // flag: a ZRL block
+                lds.lmask[b] = L;
             }
-            if (r | big) lds.bmask[b] = m | 1ull;  // flag: a special block (ZRL records or raw records)
+            cnt = (n << 16) | (1u + n + zrl + (eob ? 1u : 0u));
             // the block's MCU and slot, from the tile's (32-bit, small divisions)
             uint32_t kk;
             const uint32_t carry = udiv24(lds.tk[ti] + (uint32_t)(s0 + b), bpm, inv_bpm, kk);
-            const int k = (int)kk;
-            const uint32_t m6 = lds.tm6[ti] + carry;
+            k = (int)kk;
+            m6 = lds.tm6[ti] + carry;
             uint32_t mcol;
             const uint32_t mrow = lds.trow[ti] + udiv24(lds.tcol[ti] + carry, mw, inv_mw, mcol);
             comp = block_comp(k, bpm);
@@ -282,31 +224,13 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             } else {
                 rel = (uint32_t)(m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
             }
-            // DC difference to the chain predecessor (Image.cpp:638-678)
-            bool reset = false;
-            if (a.rst.mcus && (k == 0 || k >= (int)bpm - 2)) {
-                // exact 32-bit remainder: MCU numbers reach 2^26 (65535^2 at 4:4:4),
-                // beyond udiv24's float reciprocal (rare path: interval-boundary blocks)
-                reset = (m6 + a.rst.mcu0) % a.rst.mcus == 0;
-            }
-            // the predecessor (dc_pred_index): the previous Y slot, 3 blocks back for an
-            // MCU's first Y block, bpm back for chroma; none in the first MCU
-            const bool ynext = k >= 1 && k < (int)bpm - 2;
-            const int back = ynext ? 1 : (k == 0 ? 3 : (int)bpm);
-            const int64_t pg = (!ynext && b0 + b < bpm) ? -1 : (int64_t)(b0 + b) - back;
-            const int pd = reset ? 0 : pg < 0 ? a.seed.v[comp]
-                                   : pg >= (int64_t)b0 ? lds.dcv[pg - (int64_t)b0] : lds.prevdc[pg - ((int64_t)b0 - 6)];
-            dd = lds.dcv[b] - pd;
-            dbig = category(dd) > 10 ? 1u : 0u;
-            cnt = (n << 16) | (1u + dbig + n + (uint32_t)__builtin_popcountll(big) + zrl + (eob ? 1u : 0u));
         }
         uint32_t T;
         const uint32_t ex = block_scan<kK2Threads / 64, uint32_t, uint32_t, true, false>(cnt, lds.wsum, lane, wv, T);  // (A's barrier leads)
         if (bact) {
             lds.nzbase[b] = ex >> 16;
             lds.binfo[b] = make_uint2((rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7),
-                                      (rec0 + (ex & 0xFFFF) + 1 + dbig - (ex >> 16)) | (dbig << 30) |
-                                          (comp ? 0x80000000u : 0u));
+                                      (rec0 + (ex & 0xFFFF) + 1 - (ex >> 16)) | (comp ? 0x80000000u : 0u));
         }
         if (tid == 0) lds.tot = T >> 16;
         lds_barrier();
@@ -351,55 +275,70 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
             // zeros since the previous non-zero (or the DC): the leading zeros of the mask
             // below p, shifted to the top (p >= 1)
             int run = __builtin_clzll((m | 1ull) << (64 - p));
-            uint32_t sb = 0;  // ZRL records of the block up to and including this entry's, raw records before it
-            bool isbig = false;
-            if (m & 1ull) sb = special_before(m & ~1ull, lds.bigm[blk], p, isbig);  // (rare)
+            uint32_t zb = 0;  // ZRL records of this block up to and including this entry's
+            if (m & 1ull) {   // a ZRL block (rare): the long runs at or before p
+                for (uint64_t t = lds.lmask[blk] & (((1ull << p) - 1ull) | (1ull << p)); t; t &= t - 1) {
+                    const int q = __builtin_ctzll(t);
+                    zb += (uint32_t)(q - (63 - __builtin_clzll(m & ((1ull << q) - 1ull))) - 1) >> 4;
+                }
+            }
             const int nzr = run >> 4;
             run &= 15;
             const int cat = category(v);
             const int sym = (run << 4) | cat;
             const uint2 bi = lds.binfo[blk];
             const uint32_t acb = bi.x;
-            const uint32_t tsel = bi.y >> 31;
+            const int tsel = (int)(bi.y >> 31);
             atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + sym], 1u);
             const uint32_t kk = acb + 2u * p + 1u;
             uint32_t* kp = &lds.key[2 * tsel + 1][sym];
             if (kk < *kp) atomicMin(kp, kk);
-            const uint32_t o = (bi.y & 0x3FFFFFFFu) + e + sb;  // recbase + 1 + dbig + rank + specials
+            const uint32_t o = (bi.y & 0x7FFFFFFFu) + e + zb;  // recbase + 1 + rank + ZRLs
             if (nzr) {  // its ZRLs (F/0) just before it
                 atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256 + 0xF0], (uint32_t)nzr);
                 uint32_t* kz = &lds.key[2 * tsel + 1][0xF0];
                 if (kk - 1u < *kz) atomicMin(kz, kk - 1u);
-                for (int z = 1; z <= nzr; ++z) grec[o - z] = (uint16_t)ac_rec(2 * tsel + 1, 0xF0, 0);
+                for (int z = 1; z <= nzr; ++z) grec[o - z] = rec_word(2 * tsel + 1, 0xF0, 0);
             }
-            const uint32_t xb = extra_bits(v, cat);
-            grec[o] = (uint16_t)ac_rec(2 * tsel + 1, (uint32_t)sym, isbig ? xb >> (cat - 6) : xb);
-            if (isbig) grec[o + 1] = (uint16_t)raw_rec((uint32_t)cat - 6, xb & ((1u << (cat - 6)) - 1u));
+            grec[o] = rec_word(2 * tsel + 1, (uint32_t)sym, extra_bits(v, cat));
         }
         if (bact) {  // one lane per block: DC and EOB
             const uint64_t m = lds.bmask[b];
-            const uint32_t tsel = comp != 0;
+            const int tsel = comp != 0;
             const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7);  // text index * 128
+            // DC difference to the chain predecessor (Image.cpp:638-678)
+            int pd;
+            {
+                bool reset = false;
+                if (a.rst.mcus && (k == 0 || k >= (int)bpm - 2)) {
+                    // exact 32-bit remainder: MCU numbers reach 2^26 (65535^2 at 4:4:4),
+                    // beyond udiv24's float reciprocal (rare path: interval-boundary blocks)
+                    reset = (m6 + a.rst.mcu0) % a.rst.mcus == 0;
+                }
+                // the predecessor (dc_pred_index): the previous Y slot, 3 blocks back for an
+                // MCU's first Y block, bpm back for chroma; none in the first MCU
+                const bool ynext = k >= 1 && k < (int)bpm - 2;
+                const int back = ynext ? 1 : (k == 0 ? 3 : (int)bpm);
+                const int64_t pg = (!ynext && b0 + b < bpm) ? -1 : (int64_t)(b0 + b) - back;
+                pd = reset ? 0 : pg < 0 ? a.seed.v[block_comp(k, bpm)]
+                               : pg >= (int64_t)b0 ? lds.dcv[pg - (int64_t)b0] : lds.prevdc[pg - ((int64_t)b0 - 6)];
+            }
+            const int dd = lds.dcv[b] - pd;
             const int dcat = category(dd);
             atomicAdd(&lds.dcnt[lane & (kHistCopies - 1)][tsel * 16 + dcat], 1u);
             uint32_t* kp = &lds.key[2 * tsel][dcat];
             if (rel < *kp) atomicMin(kp, rel);
             // the block's first record (from LDS: keeping the scan results live through
             // C and D costs VGPRs)
-            const uint32_t recb = (lds.binfo[b].y & 0x3FFFFFFFu) - 1u - dbig + lds.nzbase[b];
-            const uint32_t xd = extra_bits(dd, dcat);
-            grec[recb] = (uint16_t)dc_rec(2 * tsel, (uint32_t)dcat, dbig ? xd >> (dcat - 10) : xd);
-            if (dbig) grec[recb + 1] = (uint16_t)raw_rec((uint32_t)dcat - 10, xd & ((1u << (dcat - 10)) - 1u));
+            const uint32_t recb = (lds.binfo[b].y & 0x7FFFFFFFu) - 1u + lds.nzbase[b];
+            grec[recb] = rec_word(2 * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
             if (!(m >> 63)) {  // EOB
                 atomicAdd(&lds.acnt[lane & (kHistCopies - 1)][tsel * 256], 1u);
                 uint32_t* ke = &lds.key[2 * tsel + 1][0];
                 if (acb + 127u < *ke) atomicMin(ke, acb + 127u);
-                uint32_t next = rec0 + (T & 0xFFFF);  // the next block's first record
-                if (b + 1 < nb) {
-                    const uint32_t ny = lds.binfo[b + 1].y;
-                    next = (ny & 0x3FFFFFFFu) - 1u - ((ny >> 30) & 1u) + lds.nzbase[b + 1];
-                }
-                grec[next - 1] = (uint16_t)ac_rec(2 * tsel + 1, 0, 0);  // the block's last record
+                const uint32_t eo = (b + 1 < nb ? (lds.binfo[b + 1].y & 0x7FFFFFFFu) - 1u + lds.nzbase[b + 1]
+                                                : rec0 + (T & 0xFFFF)) - 1;  // the block's last record
+                grec[eo] = rec_word(2 * tsel + 1, 0, 0);
             }
         }
         JPGE_ACC(3, tq);
