@@ -215,18 +215,21 @@ class HashOrder {
     }
 };
 
-struct HeapItem {
-    int w;
-    int node;
-};
+// A heap item: weight in the high word, node id in the low word.  Comparisons look at
+// the weight only (as the reference's comparator), so equal weights never reorder.
+using HeapItem = uint64_t;
+inline HeapItem item(int w, int node) { return ((uint64_t)(uint32_t)w << 32) | (uint32_t)node; }
+inline int item_w(HeapItem x) { return (int)(x >> 32); }
+inline int item_node(HeapItem x) { return (int)(uint32_t)x; }
 // std::push_heap with comp(a, b) = a.w > b.w (libstdc++ __push_heap)
 inline void heap_push(HeapItem* h, int& size, HeapItem v) {
     int hole = size++;
-    int parent = (hole - 1) / 2;
-    while (hole > 0 && h[parent].w > v.w) {
+    const int vw = item_w(v);
+    while (hole > 0) {
+        const int parent = (hole - 1) / 2;
+        if (!(item_w(h[parent]) > vw)) break;
         h[hole] = h[parent];
         hole = parent;
-        parent = (hole - 1) / 2;
     }
     h[hole] = v;
 }
@@ -237,9 +240,10 @@ inline HeapItem heap_pop(HeapItem* h, int& size) {
     if (len > 0) {
         const HeapItem v = h[len];
         int hole = 0, child = 0;
-        while (child < (len - 1) / 2) {
+        const int lim = (len - 1) / 2;
+        while (child < lim) {  // (a trip count fixed by len; the child choice is a select)
             child = 2 * (child + 1);
-            if (h[child].w > h[child - 1].w) --child;
+            child -= (int)(item_w(h[child]) > item_w(h[child - 1]));
             h[hole] = h[child];
             hole = child;
         }
@@ -248,11 +252,12 @@ inline HeapItem heap_pop(HeapItem* h, int& size) {
             h[hole] = h[child - 1];
             hole = child - 1;
         }
-        int parent = (hole - 1) / 2;
-        while (hole > 0 && h[parent].w > v.w) {
+        const int vw = item_w(v);
+        while (hole > 0) {
+            const int parent = (hole - 1) / 2;
+            if (!(item_w(h[parent]) > vw)) break;
             h[hole] = h[parent];
             hole = parent;
-            parent = (hole - 1) / 2;
         }
         h[hole] = v;
     }
@@ -279,11 +284,12 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     // package-merge, Huffman.hpp:114-174: 15 levels, each a copy of the leaves' heap
     // plus the previous level's packages; levels[15] starts empty
     constexpr int kLevels = 15, kCap = 2 * kMaxSyms;
+    constexpr int kMaxKids = kLevels * kCap, kMaxNodes = kMaxSyms + kMaxKids;
     HeapItem base[kMaxSyms], cur[kCap], nxt[kCap];
     int nbase = 0;
-    for (int i = 0; i < n; ++i) heap_push(base, nbase, HeapItem{lcnt[i], i});
-    static thread_local std::vector<std::pair<int, int>> kids;
-    kids.clear();
+    for (int i = 0; i < n; ++i) heap_push(base, nbase, item(lcnt[i], i));
+    static thread_local int kid_a[kMaxKids], kid_b[kMaxKids], mult[kMaxNodes], first[kMaxNodes];
+    int nkids = 0;
     int ncur = nbase;
     std::copy(base, base + nbase, cur);
     for (int lv = 0; lv < kLevels; ++lv) {
@@ -294,30 +300,31 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         }
         while (ncur > 1) {
             const HeapItem a = heap_pop(cur, ncur), b = heap_pop(cur, ncur);
-            kids.emplace_back(a.node, b.node);
-            heap_push(nxt, nn, HeapItem{a.w + b.w, n + (int)kids.size() - 1});
+            kid_a[nkids] = item_node(a);
+            kid_b[nkids] = item_node(b);
+            heap_push(nxt, nn, item(item_w(a) + item_w(b), n + nkids));
+            ++nkids;
         }
         std::copy(nxt, nxt + nn, cur);
         ncur = nn;
     }
     // cur: levels[15]; pop order = the final packages.  Push the multiplicities and the
     // first final package down the DAG (a package's id exceeds its children's).
-    const int total = n + (int)kids.size();
-    static thread_local std::vector<int> mult, first;
-    mult.assign(total, 0);
-    first.assign(total, INT32_MAX);
+    const int total = n + nkids;
+    std::fill(mult, mult + total, 0);
+    std::fill(first, first + total, INT32_MAX);
     for (int k = 0; ncur > 0; ++k) {
-        const int f = heap_pop(cur, ncur).node;
+        const int f = item_node(heap_pop(cur, ncur));
         mult[f] += 1;
         if (k < first[f]) first[f] = k;
     }
     for (int id = total - 1; id >= n; --id) {
         if (!mult[id]) continue;
-        const auto& kk = kids[id - n];
-        mult[kk.first] += mult[id];
-        mult[kk.second] += mult[id];
-        if (first[id] < first[kk.first]) first[kk.first] = first[id];
-        if (first[id] < first[kk.second]) first[kk.second] = first[id];
+        const int ka = kid_a[id - n], kb = kid_b[id - n];
+        mult[ka] += mult[id];
+        mult[kb] += mult[id];
+        if (first[id] < first[ka]) first[ka] = first[id];
+        if (first[id] < first[kb]) first[kb] = first[id];
     }
     // code_lengths (an unordered_map) receives symbols by (first package, symbol)
     int ins[kMaxSyms];
