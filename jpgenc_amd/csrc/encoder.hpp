@@ -167,7 +167,8 @@ class Encoder {
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables (JPGE_INLINE_TABLES=0)
-    bool inline_tables_ = true; // JPGE_INLINE_TABLES: each lane's thread builds its frames' tables (no pool)
+    int inline_tables_ = 2;     // JPGE_INLINE_TABLES: 1 each lane's thread builds its frames' tables, 0 the
+                                // pool, 2 (default) by frame size (encoder.cpp kInlineTablesMinPixels)
     int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
     // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
     // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
