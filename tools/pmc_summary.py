@@ -11,6 +11,7 @@ import argparse
 import collections
 import csv
 import glob
+import gzip
 import json
 import re
 
@@ -22,8 +23,11 @@ def short(name):
 
 def load(d):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
-        for r in csv.DictReader(open(f)):
+    files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+    files += glob.glob(f"{d}/**/*counter_collection.csv.gz", recursive=True)
+    for f in sorted(files):
+        fh = gzip.open(f, "rt") if f.endswith(".gz") else open(f)
+        for r in csv.DictReader(fh):
             agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
