@@ -301,8 +301,20 @@ def thread_cpu() -> dict:
     return out
 
 
+def thread_report(th0: dict, dt: float):
+    """Diagnostic (JPGE_BENCH_THREADS): each thread's CPUs over the timed region, to stderr."""
+    if not th0:
+        return
+    th1 = thread_cpu()
+    use = collections.Counter()
+    for k, v in th1.items():
+        use[k] += (v - th0.get(k, 0.0)) / dt
+    print(f"threads: {len(th1)}; busiest:", {f"{k[1]}/{k[0]}": round(v, 2) for k, v in use.most_common(24)},
+          file=sys.stderr)
+
+
 class ThreadSampler:
-    """Diagnostic (JPGE_BENCH_THREADS): samples every thread's scheduler state and
+    """Diagnostic (JPGE_BENCH_THREADS=2): samples every thread's scheduler state and
     kernel wait channel every 2 ms; stop() prints each busy thread's distribution."""
 
     def __init__(self):
@@ -582,6 +594,7 @@ def run_batch1080(args, rank, local, world, pg):
     torch.cuda.synchronize()
     barrier(pg)
     cg0 = cgroup_cpu_stat()
+    th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         lens = step()
@@ -589,6 +602,7 @@ def run_batch1080(args, rank, local, world, pg):
     barrier(pg)
     dt = time.perf_counter() - t0
     cg1 = cgroup_cpu_stat()
+    thread_report(th0, dt)
     dt_max = max_over_ranks(pg, dt)
     nbytes = sum_over_ranks(pg, float(sum(lens)))
     # verification: every frame of the last step, as rank 0 holds it, equals the
@@ -669,7 +683,7 @@ def run_frames(args, rank, local, world, pg):
     step_t = []
     cg0 = cgroup_cpu_stat()
     th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
-    sampler = ThreadSampler() if th0 else None
+    sampler = ThreadSampler() if os.environ.get("JPGE_BENCH_THREADS") == "2" else None
     for _ in range(args.steps):
         ts = time.perf_counter()
         lens = enc.encode_batch_dev(frames, outd, quality=args.quality)
@@ -682,13 +696,7 @@ def run_frames(args, rank, local, world, pg):
     cg1 = cgroup_cpu_stat()
     if sampler:
         sampler.stop()
-    if th0:
-        th1 = thread_cpu()
-        use = collections.Counter()
-        for k, v in th1.items():
-            use[k] += (v - th0.get(k, 0.0)) / dt
-        print(f"threads: {len(th1)}; busiest:", {f"{k[1]}/{k[0]}": round(v, 2) for k, v in use.most_common(24)},
-              file=sys.stderr)
+    thread_report(th0, dt)
     tm = enc.timing()
     enc.set_timing(False)
 

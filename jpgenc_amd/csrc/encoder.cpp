@@ -73,16 +73,36 @@ inline hipError_t wait_event(hipEvent_t e) {
 // which costs the GPU ~6 us of idle each time.  `queued`: set once the kernel that
 // writes the word is on the stream (another thread launches it); before that an
 // idle stream is no error.
+//
+// `guess` (napping waits): a running estimate of how long this wait takes at its call
+// site.  The first sleep covers most of it in one wake-up, and naps poll the rest, so
+// a wait of ~100 us costs two or three wake-ups instead of ten.
+struct WaitGuess {
+    double ema_us = 0;  // smoothed wait duration (0: none yet)
+    double frac = 0;    // first sleep = frac * ema (0: off)
+};
 inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int nap_us = 0,
-                    const std::atomic<int>* queued = nullptr) {
+                    const std::atomic<int>* queued = nullptr, WaitGuess* guess = nullptr) {
     const bool nap = nap_us > 0;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto next_query = t0 + std::chrono::milliseconds(2);
     clk::time_point idle_since{};  // the stream was first seen idle without the word
     bool idle = false;
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
+        if (guess) guess->ema_us *= 0.85;
+        return kOk;
+    }
+    if (nap && guess && guess->frac > 0 && guess->ema_us > 3.0 * nap_us)
+        std::this_thread::sleep_for(std::chrono::microseconds((long)(guess->frac * guess->ema_us)));
     for (uint32_t spins = 0;; ++spins) {
-        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return kOk;
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
+            if (guess) {
+                const double us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+                guess->ema_us = guess->ema_us > 0 ? 0.85 * guess->ema_us + 0.15 * us : us;
+            }
+            return kOk;
+        }
         if (nap) std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
         if (!nap && (spins & 255) != 255) continue;
         const auto now = clk::now();
@@ -164,11 +184,13 @@ struct HostHist {  // written by hist_export_kernel into mapped pinned memory
 // whose histograms are in (with several lanes, jobs finish out of order).
 class Encoder::TablePool {
   public:
+    using clk = std::chrono::steady_clock;
     struct Job {
         std::function<bool()> ready;
         std::function<void()> run;
+        clk::time_point submit;
     };
-    explicit TablePool(int n) {
+    explicit TablePool(int n, double first_sleep) : frac_(first_sleep) {
         for (int i = 0; i < n; ++i)
             th_.emplace_back([this, i] {
                 prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // ~1 us sleeps while polling
@@ -186,6 +208,7 @@ class Encoder::TablePool {
         for (auto& t : th_) t.join();
     }
     void submit(Job job) {
+        job.submit = clk::now();
         {
             std::lock_guard<std::mutex> g(mu_);
             q_.push_back(std::move(job));
@@ -194,6 +217,10 @@ class Encoder::TablePool {
     }
 
   private:
+    // One worker at a time polls for a ready job (the others wait on the condition
+    // variable): it sleeps until the earliest job is likely ready (its submit time plus
+    // frac_ of the usual submit-to-ready delay), then naps ~10 us between looks.  (Every
+    // worker napping on its own cost ~0.8 CPU per worker with 1080p frames.)
     void loop() {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
@@ -202,18 +229,35 @@ class Encoder::TablePool {
                 cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
                 continue;
             }
+            const auto now = clk::now();
             auto it = std::find_if(q_.begin(), q_.end(), [](const Job& j) { return j.ready(); });
-            if (it == q_.end()) {  // nothing ready: nap ~10 us and look again
+            if (it != q_.end()) {
+                const double us = std::chrono::duration<double, std::micro>(now - it->submit).count();
+                ready_us_ = ready_us_ > 0 ? 0.85 * ready_us_ + 0.15 * us : us;
+                std::function<void()> run = std::move(it->run);
+                q_.erase(it);
+                if (!q_.empty()) cv_.notify_one();  // (someone polls for the rest)
                 lk.unlock();
-                std::this_thread::sleep_for(std::chrono::microseconds(10));
+                run();
                 lk.lock();
                 continue;
             }
-            std::function<void()> run = std::move(it->run);
-            q_.erase(it);
+            if (polling_) {  // another worker polls
+                cv_.wait(lk);
+                continue;
+            }
+            polling_ = true;
+            auto wake = now + std::chrono::microseconds(10);
+            if (frac_ > 0 && ready_us_ > 0) {
+                auto first = q_.front().submit;
+                for (const Job& j : q_) first = std::min(first, j.submit);
+                const auto due = first + std::chrono::microseconds((long)(frac_ * ready_us_));
+                if (due > wake) wake = due;
+            }
             lk.unlock();
-            run();
+            std::this_thread::sleep_until(wake);
             lk.lock();
+            polling_ = false;
         }
     }
     std::vector<std::thread> th_;
@@ -221,6 +265,9 @@ class Encoder::TablePool {
     std::condition_variable cv_;
     std::deque<Job> q_;
     bool stop_ = false;
+    bool polling_ = false;
+    double frac_ = 0;      // first sleep, of the usual submit-to-ready delay
+    double ready_us_ = 0;  // smoothed submit-to-ready delay of the jobs (upper bound: when first seen ready)
 };
 
 struct Encoder::Slot {
@@ -270,6 +317,9 @@ struct Encoder::Slot {
     uint32_t img_w = 0, img_h = 0;
     int tables_status = 0;
     bool inline_tables = false;  // this frame's tables are built by its lane's thread (else the pool)
+    // the lane's wait estimates (histograms when its own thread builds the tables; results)
+    WaitGuess* guess_hist = nullptr;
+    WaitGuess* guess_result = nullptr;
 
     ~Slot() {
         hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
@@ -295,6 +345,7 @@ struct Encoder::Lane {
     int result = 0;
     std::atomic<uint32_t> posted{0}, finished{0};
     std::atomic<bool> stop{false};
+    WaitGuess guess_hist, guess_result;  // (the slots point here)
 
     void start() {
         th = std::thread([this] {
@@ -382,6 +433,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
     e->inline_tables_ = env_int("JPGE_INLINE_TABLES", 2, 0, 2);
     e->nap_us_ = env_int("JPGE_NAP_US", e->nap_us_, 1, 1000);
+    e->first_sleep_ = env_int("JPGE_FIRST_SLEEP", (int)(e->first_sleep_ * 100 + 0.5), 0, 95) / 100.0;
     const int nap = env_int("JPGE_NAP", -1, -1, 1);
     e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
     e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
@@ -409,9 +461,12 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
         ln->id = l;
         JPGE_HIP(hipStreamCreateWithFlags(&ln->stream, hipStreamNonBlocking));
         JPGE_HIP(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
+        ln->guess_hist.frac = ln->guess_result.frac = e->first_sleep_;
         for (int i = 0; i < nslots; ++i) {
             std::unique_ptr<Slot> s(new Slot());
             s->stream = ln->stream;
+            s->guess_hist = &ln->guess_hist;
+            s->guess_result = &ln->guess_result;
             for (int k = 0; k < 8; ++k)
                 JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], hipEventDefault));
             JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
@@ -667,7 +722,8 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel) {
-    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : 10), &s.export_queued))
+    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : 10), &s.export_queued,
+                               s.inline_tables ? s.guess_hist : nullptr))
         return w;
     uint32_t cnt[1024];
     uint64_t first[1024];
@@ -738,7 +794,7 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
 }
 
 int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
-    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0)) return w;
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, s.guess_result)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[7]));
         std::lock_guard<std::mutex> g(times_mu_);
@@ -794,7 +850,7 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
-    if (inline_tables_ != 1 && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_));
+    if (inline_tables_ != 1 && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_, first_sleep_));
     // Frames are dealt dynamically: a lane takes the batch's next frame when its
     // pipeline has room, so lanes finish together.  Lane 0 runs on the calling thread.
     const int nl = std::min<int>((int)lanes_.size(), n);
@@ -879,7 +935,8 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
                                sp->tables_status = build_tables(*sp, false);
                                sp->t_done = std::chrono::steady_clock::now();
                                sp->tables_done.store(1, std::memory_order_release);
-                           }});
+                           },
+                           {}});
         } else {
             s.tables_status = build_tables(s, true);
             s.tables_done.store(1, std::memory_order_release);

@@ -170,6 +170,7 @@ class Encoder {
     int inline_tables_ = 2;     // JPGE_INLINE_TABLES: 1 each lane's thread builds its frames' tables, 0 the
                                 // pool, 2 (default) by frame size (encoder.cpp kInlineTablesMinPixels)
     int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
+    double first_sleep_ = 0.7;  // JPGE_FIRST_SLEEP (percent): a lane's first sleep in a wait, of its usual length
     // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
     // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
     // lanes (one small launch instead of every pack workgroup scanning all records:

@@ -233,24 +233,34 @@ inline void heap_push(HeapItem* h, int& size, HeapItem v) {
     }
     h[hole] = v;
 }
-// std::pop_heap + pop_back (libstdc++ __pop_heap / __adjust_heap / __push_heap)
+// std::pop_heap + pop_back (libstdc++ __pop_heap / __adjust_heap / __push_heap).
+// __adjust_heap walks the hole from the root to the bottom, at each node taking the
+// right child unless the left one is lighter.  The walk keeps the two children of the
+// hole in registers and loads their four children one step ahead, so a step waits on
+// a compare, not on a load (the heap arrays carry kHeapPad slack for those loads).
+constexpr int kHeapPad = 8;
 inline HeapItem heap_pop(HeapItem* h, int& size) {
     const HeapItem top = h[0];
     const int len = size - 1;
     if (len > 0) {
         const HeapItem v = h[len];
-        int hole = 0, child = 0;
+        int hole = 0;
         const int lim = (len - 1) / 2;
-        while (child < lim) {  // (a trip count fixed by len; the child choice is a select)
-            child = 2 * (child + 1);
-            child -= (int)(item_w(h[child]) > item_w(h[child - 1]));
-            h[hole] = h[child];
-            hole = child;
+        if (hole < lim) {
+            HeapItem cl = h[1], cr = h[2];
+            do {
+                const HeapItem* g = h + 4 * hole + 3;  // the children's children (may lie past len)
+                const HeapItem g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3];
+                const bool left = item_w(cr) > item_w(cl);
+                h[hole] = left ? cl : cr;
+                hole = 2 * hole + 2 - (int)left;
+                cl = left ? g0 : g2;
+                cr = left ? g1 : g3;
+            } while (hole < lim);
         }
-        if ((len & 1) == 0 && child == (len - 2) / 2) {
-            child = 2 * (child + 1);
-            h[hole] = h[child - 1];
-            hole = child - 1;
+        if ((len & 1) == 0 && hole == (len - 2) / 2) {
+            h[hole] = h[2 * hole + 1];
+            hole = 2 * hole + 1;
         }
         const int vw = item_w(v);
         while (hole > 0) {
@@ -285,7 +295,9 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     // plus the previous level's packages; levels[15] starts empty
     constexpr int kLevels = 15, kCap = 2 * kMaxSyms;
     constexpr int kMaxKids = kLevels * kCap, kMaxNodes = kMaxSyms + kMaxKids;
-    HeapItem base[kMaxSyms], cur[kCap], nxt[kCap];
+    // (two level buffers, swapped; padded for heap_pop's look-ahead loads)
+    static thread_local HeapItem base[kMaxSyms], buf0[2 * kCap + kHeapPad], buf1[2 * kCap + kHeapPad];
+    HeapItem *cur = buf0, *nxt = buf1;
     int nbase = 0;
     for (int i = 0; i < n; ++i) heap_push(base, nbase, item(lcnt[i], i));
     static thread_local int kid_a[kMaxKids], kid_b[kMaxKids], mult[kMaxNodes], first[kMaxNodes];
@@ -305,7 +317,7 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
             heap_push(nxt, nn, item(item_w(a) + item_w(b), n + nkids));
             ++nkids;
         }
-        std::copy(nxt, nxt + nn, cur);
+        std::swap(cur, nxt);
         ncur = nn;
     }
     // cur: levels[15]; pop order = the final packages.  Push the multiplicities and the
