@@ -80,6 +80,9 @@ inline hipError_t wait_event(hipEvent_t e) {
 struct WaitGuess {
     double ema_us = 0;  // smoothed wait duration (0: none yet)
     double frac = 0;    // first sleep = frac * ema (0: off)
+    // statistics (JPGE_CPU_PROF): waits, waits already satisfied on entry, naps, total us
+    uint64_t waits = 0, ready = 0, naps = 0;
+    double total_us = 0;
 };
 inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int nap_us = 0,
                     const std::atomic<int>* queued = nullptr, WaitGuess* guess = nullptr) {
@@ -89,21 +92,31 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int 
     auto next_query = t0 + std::chrono::milliseconds(2);
     clk::time_point idle_since{};  // the stream was first seen idle without the word
     bool idle = false;
+    if (guess) ++guess->waits;
     if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
-        if (guess) guess->ema_us *= 0.85;
+        if (guess) {
+            guess->ema_us *= 0.85;
+            ++guess->ready;
+        }
         return kOk;
     }
-    if (nap && guess && guess->frac > 0 && guess->ema_us > 3.0 * nap_us)
+    if (nap && guess && guess->frac > 0 && guess->ema_us > 3.0 * nap_us) {
         std::this_thread::sleep_for(std::chrono::microseconds((long)(guess->frac * guess->ema_us)));
+        ++guess->naps;
+    }
     for (uint32_t spins = 0;; ++spins) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
             if (guess) {
                 const double us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
                 guess->ema_us = guess->ema_us > 0 ? 0.85 * guess->ema_us + 0.15 * us : us;
+                guess->total_us += us;
             }
             return kOk;
         }
-        if (nap) std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+        if (nap) {
+            std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+            if (guess) ++guess->naps;
+        }
         if (!nap && (spins & 255) != 255) continue;
         const auto now = clk::now();
         if (now < next_query) continue;
@@ -428,6 +441,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     if (const char* sw = std::getenv("JPGE_STATS_WGS")) e->stats_wgs_ = (uint32_t)std::strtoul(sw, nullptr, 10);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
+    e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
@@ -486,6 +500,27 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
 }
 
 Encoder::~Encoder() {
+    if (cpu_prof_ && cpu_frames_.load()) {
+        const double f = (double)cpu_frames_.load();
+        std::fprintf(stderr, "jpge cpu per frame (us): tables %.2f launch-1 %.2f launch-entropy %.2f finish %.2f "
+                             "loop-top %.2f end %.2f\n",
+                     cpu_ns_[1] / f / 1e3, cpu_ns_[2] / f / 1e3, cpu_ns_[3] / f / 1e3, cpu_ns_[4] / f / 1e3,
+                     cpu_ns_[0] / f / 1e3, cpu_ns_[5] / f / 1e3);
+        if (cpu_builds_.load())
+            std::fprintf(stderr, "jpge table builds: %lld, histogram read %.2f us, tables + headers %.2f us each\n",
+                         (long long)cpu_builds_.load(), cpu_read_ns_.load() / 1e3 / cpu_builds_.load(),
+                         cpu_build_ns_.load() / 1e3 / cpu_builds_.load());
+        if (cpu_builds_.load())
+            std::fprintf(stderr, "jpge   of which: 4 tables %.2f us, code words to mapped memory %.2f us, headers %.2f us\n",
+                         cpu_part_ns_[0].load() / 1e3 / cpu_builds_.load(), cpu_part_ns_[1].load() / 1e3 / cpu_builds_.load(),
+                         cpu_part_ns_[2].load() / 1e3 / cpu_builds_.load());
+        for (auto& ln : lanes_)
+            for (const WaitGuess* g : {&ln->guess_hist, &ln->guess_result})
+                std::fprintf(stderr, "jpge lane %d %s waits: %llu (%llu ready on entry), %.2f naps and %.1f us per wait, ema %.1f\n",
+                             ln->id, g == &ln->guess_hist ? "histogram" : "result", (unsigned long long)g->waits,
+                             (unsigned long long)g->ready, g->waits ? (double)g->naps / g->waits : 0.0,
+                             g->waits ? g->total_us / g->waits : 0.0, g->ema_us);
+    }
     for (auto& ln : lanes_) ln->shutdown();
     for (auto& b : scratch_) hipFree(b.first);
     pool_.reset();  // (no jobs are pending between calls)
@@ -725,27 +760,47 @@ int Encoder::build_tables(Slot& s, bool parallel) {
     if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : 10), &s.export_queued,
                                s.inline_tables ? s.guess_hist : nullptr))
         return w;
+    auto thread_ns = [] {
+        timespec t;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+        return (int64_t)t.tv_sec * 1000000000 + t.tv_nsec;
+    };
+    const int64_t t0 = cpu_prof_ ? thread_ns() : 0;
     uint32_t cnt[1024];
     uint64_t first[1024];
     for (int i = 0; i < 1024; ++i) {
         cnt[i] = s.h_hist->cnt[i];
         first[i] = ~s.h_hist->key[i];
     }
-    return build_tables_from(s, cnt, first, parallel);
+    const int64_t t1 = cpu_prof_ ? thread_ns() : 0;
+    const int r = build_tables_from(s, cnt, first, parallel);
+    if (cpu_prof_) {
+        cpu_read_ns_.fetch_add(t1 - t0, std::memory_order_relaxed);
+        cpu_build_ns_.fetch_add(thread_ns() - t1, std::memory_order_relaxed);
+        cpu_builds_.fetch_add(1, std::memory_order_relaxed);
+    }
+    return r;
 }
 
 // The four tables from counts and first-occurrence keys, and the headers (the
 // image's real dimensions in SOF0), into the slot's pinned staging buffer.
 int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t* first_all, bool parallel) {
+    auto thread_ns = [] {
+        timespec t;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+        return (int64_t)t.tv_sec * 1000000000 + t.tv_nsec;
+    };
+    const int64_t t0 = cpu_prof_ ? thread_ns() : 0;
     HuffTable tabs[4];
     int ok[4] = {0, 0, 0, 0};
     // the four tables are independent; the AC tables dominate
-    parallel_for(4, parallel ? 4 : 1, [&](long t) {
-        if (!build_table(cnt_all + t * 256, first_all + t * 256, tabs[t])) return;
-        for (int i = 0; i < 256; ++i)
-            s.h_tab[t * 256 + i] = ((uint32_t)tabs[t].len[i] << 16) | (tabs[t].code[i] & 0xFFFF);
-        ok[t] = 1;
-    });
+    parallel_for(4, parallel ? 4 : 1, [&](long t) { ok[t] = build_table(cnt_all + t * 256, first_all + t * 256, tabs[t]); });
+    const int64_t t1 = cpu_prof_ ? thread_ns() : 0;
+    for (int t = 0; t < 4; ++t)
+        if (ok[t])
+            for (int i = 0; i < 256; ++i)
+                s.h_tab[t * 256 + i] = ((uint32_t)tabs[t].len[i] << 16) | (tabs[t].code[i] & 0xFFFF);
+    const int64_t t2 = cpu_prof_ ? thread_ns() : 0;
     const int bad = !(ok[0] & ok[1] & ok[2] & ok[3]);
     uint64_t nsym = 0;
     for (int i = 0; i < 1024; ++i) nsym += cnt_all[i];
@@ -768,6 +823,11 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     if (hdr.size() > kHdrMax) return kErrInternal;
     std::memcpy(reinterpret_cast<uint8_t*>(s.h_tab) + kTabBytes, hdr.data(), hdr.size());
     s.hdr_len = hdr.size();
+    if (cpu_prof_) {
+        cpu_part_ns_[0].fetch_add(t1 - t0, std::memory_order_relaxed);
+        cpu_part_ns_[1].fetch_add(t2 - t1, std::memory_order_relaxed);
+        cpu_part_ns_[2].fetch_add(thread_ns() - t2, std::memory_order_relaxed);
+    }
     if (s.out_cap && s.out_cap < s.hdr_len + 2) return kErrNoSpace;
     return kOk;
 }
@@ -949,7 +1009,21 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
     auto us = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::micro>(t - t_call).count();
     };
+    // diagnostic (JPGE_CPU_PROF): this thread's CPU time per loop segment, summed per encoder
+    int64_t cpu_last = 0;
+    int64_t cpu_acc[6] = {0, 0, 0, 0, 0, 0};
+    auto thread_ns = [] {
+        timespec t;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+        return (int64_t)t.tv_sec * 1000000000 + t.tv_nsec;
+    };
+    if (cpu_prof_) cpu_last = thread_ns();
     auto mark = [&](int i, int point, const Slot* job = nullptr) {
+        if (cpu_prof_) {
+            const int64_t t = thread_ns();
+            cpu_acc[point] += t - cpu_last;
+            cpu_last = t;
+        }
         if (host_trace_file_)
             trace.push_back({(double)i, (double)point, us(std::chrono::steady_clock::now()),
                              job ? us(job->t_submit) : 0.0, job ? us(job->t_start) : 0.0,
@@ -1032,6 +1106,10 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         else JPGE_HIP(wait_event(ln.done));
     }
     mark(n + L + D, 5);  // (n: this lane's frame count)
+    if (cpu_prof_) {
+        for (int k = 0; k < 6; ++k) cpu_ns_[k].fetch_add(cpu_acc[k], std::memory_order_relaxed);
+        cpu_frames_.fetch_add(n, std::memory_order_relaxed);
+    }
     if (host_trace_file_) {
         std::lock_guard<std::mutex> g(trace_mu_);
         if (FILE* f = std::fopen(host_trace_file_, "a")) {

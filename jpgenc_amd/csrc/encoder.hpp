@@ -180,6 +180,10 @@ class Encoder {
     int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
     bool nap_ = false;          // lane threads sleep ~10 us between polls instead of spinning (default: >1 lane; JPGE_NAP)
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
+    bool cpu_prof_ = false;                  // JPGE_CPU_PROF: lane threads' CPU per loop segment (printed at close)
+    std::atomic<int64_t> cpu_ns_[6] = {};
+    std::atomic<int64_t> cpu_frames_{0};
+    std::atomic<int64_t> cpu_read_ns_{0}, cpu_build_ns_{0}, cpu_builds_{0}, cpu_part_ns_[3] = {};
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
     uint64_t* d_dbg_ = nullptr;
     size_t dbg_words_ = 0;
