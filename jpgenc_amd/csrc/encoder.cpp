@@ -439,6 +439,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
     if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     if (const char* sw = std::getenv("JPGE_STATS_WGS")) e->stats_wgs_ = (uint32_t)std::strtoul(sw, nullptr, 10);
+    e->fdct_wgs_ = (uint32_t)env_int("JPGE_FDCT_WGS", 0, 0, 65536);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
     e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
@@ -541,7 +542,7 @@ void Encoder::dump_stamps(const Slot& s) {
     if (!stamps_file_ || !d_dbg_) return;
     std::vector<uint64_t> h(dbg_words_);
     if (hipMemcpy(h.data(), d_dbg_, dbg_words_ * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1), stats_grid(layout(s.g), stats_wgs()), layout(s.g).grid(),
+    const uint64_t hdr[4] = {fdct_grid(s.g, lanes_.size() == 1, fdct_wgs_), stats_grid(layout(s.g), stats_wgs()), layout(s.g).grid(),
                              layout(s.g).grid()};
     FILE* f = std::fopen(stamps_file_, "wb");
     if (!f) return;
@@ -607,6 +608,7 @@ FdctArgs Encoder::fdct_args(Slot& s, int maxval, Slot* imp) {
     a.g = s.g;
     a.maxval = maxval;
     a.solo = lanes_.size() == 1;  // (several lanes: K1 runs beside other frames' kernels)
+    a.wgs = fdct_wgs_;
     for (int i = 0; i < 64; ++i) {
         a.q[i] = s.qy[i];
         a.q[64 + i] = s.qc[i];
@@ -640,7 +642,7 @@ StatsArgs Encoder::stats_args(Slot& s) {
     if (!stats_wgs_ && lanes_.size() > 1) {
         // frames under ~3 MPix (fewer than 3 tiles per workgroup at 384): about 3 tiles per
         // workgroup, not one each (a workgroup's fixed costs, its first load not overlapped:
-        // 1080p batch +9%); 4K and larger keep the 2-per-CU grid
+        // 1080p batch +9%); 4K and larger keep one workgroup per CU (stats_wgs)
         const uint32_t t = seg_tiles(st.seg);
         if (t < 3u * 384u) st.wgs = std::max(1u, (t + 2) / 3);
     }

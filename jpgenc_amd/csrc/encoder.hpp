@@ -156,21 +156,25 @@ class Encoder {
     // entropy workgroups: the override, else 512 for a single lane (its frames' latency:
     // -5 us at 4K) and seg_layout's default (384) beside other lanes (+3% throughput)
     uint32_t entropy_wgs() const { return entropy_wgs_ ? entropy_wgs_ : (lanes_.size() == 1 ? 512u : 0u); }
-    // statistics workgroups: 3 per CU alone (the shortest runs), 2 per CU beside other
-    // lanes (longer runs, fewer resident workgroups: measured +0.8% in the pipeline
-    // over 3 per CU; 1.5 per CU equal, 2.5 or 1 per CU slower)
-    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 0u : 512u); }
+    // statistics workgroups: 3 per CU alone (the shortest runs), 1 per CU beside other
+    // lanes (6 tiles per workgroup at 4K: its fixed costs, the prologue, first load and
+    // flush, amortised; 256 vs 512: +1.6% in the pipeline, 1.25, 1.5 and 0.75 per CU slower)
+    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 0u : 256u); }
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
     // the entropy partition a slot's current frame runs on
     SegLayout slot_layout(const Slot& s) const;
     uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
+    uint32_t fdct_wgs_ = 0;     // JPGE_FDCT_WGS: pipeline transform grid (0: fdct_grid's cap)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables (JPGE_INLINE_TABLES=0)
     int inline_tables_ = 2;     // JPGE_INLINE_TABLES: 1 each lane's thread builds its frames' tables, 0 the
                                 // pool, 2 (default) by frame size (encoder.cpp kInlineTablesMinPixels)
     int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
-    double first_sleep_ = 0.7;  // JPGE_FIRST_SLEEP (percent): a lane's first sleep in a wait, of its usual length
+    // JPGE_FIRST_SLEEP (percent, default off): a lane's first sleep in a wait, of its usual
+    // length.  At 70%: 4K host CPU 1.8 -> 1.7 at equal throughput, but 16384^2 frames (4 per
+    // lane per batch, irregular waits) lost 14% to oversleeping.
+    double first_sleep_ = 0;
     // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
     // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
     // lanes (one small launch instead of every pack workgroup scanning all records:

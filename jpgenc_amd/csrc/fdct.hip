@@ -665,12 +665,12 @@ void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t
     }
 }
 
-uint32_t fdct_grid(const Geometry& g, bool solo) {
+uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs) {
     const uint32_t per = g.row8() ? 16 / g.yh : 4;  // MCUs per tile
     const uint32_t tiles = ((g.mw + per - 1) / per) * g.mh;
     // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
     const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
-    const uint32_t cap = solo ? 256u * (16u / (uint32_t)kK1WavesSolo) : (uint32_t)K1_SHARED_CAP;
+    const uint32_t cap = solo ? 256u * (16u / (uint32_t)kK1WavesSolo) : override_wgs ? override_wgs : (uint32_t)K1_SHARED_CAP;
     return wgs < cap ? wgs : cap;
 }
 
@@ -678,7 +678,7 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
     // 32-bit buffer offsets: the frame's pixels and coefficients must stay below kOob
     // (a 16384^2 frame needs 805 MB of each)
     if ((uint64_t)a.stride * a.g.height >= kOob || (uint64_t)a.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
-    const uint32_t grid = fdct_grid(a.g, a.solo);
+    const uint32_t grid = fdct_grid(a.g, a.solo, a.wgs);
     // the kernels assume these shapes (kernels.hpp Geometry)
     if (a.g.row8()) {
         switch (a.g.yh) {

@@ -72,6 +72,7 @@ struct FdctArgs {
     Geometry g;
     int maxval;      // 255 -> exact integer colour path
     bool solo;       // the kernel has the GPU to itself: whole-CU workgroups (else 4-wave ones)
+    uint32_t wgs;    // pipeline grid override (0: the default cap; experiments, JPGE_FDCT_WGS)
     // luma then chroma quantisers, natural order (bytes: a small kernarg block; 16-byte
     // aligned so the kernels fetch it with scalar loads, see fdct.hip q_entry)
     alignas(16) uint8_t q[128];
@@ -265,7 +266,7 @@ struct KTimer {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
-uint32_t fdct_grid(const Geometry& g, bool solo);
+uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs = 0);
 // statistics workgroups: wgs (0: 3 per CU), within the tile-table bound and the tile count
 uint32_t stats_grid(const SegLayout& L, uint32_t wgs = 0);
 // entropy partition of a frame: restart_mcus = 0 -> one segment over 128-block tiles
