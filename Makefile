@@ -23,8 +23,9 @@ DIAG_OBJS := $(addprefix $(BUILD)/diag/,$(DEV_SRCS:.hip=.o))
 HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h
 FACADE_TEST := tests/cpp/bin/test_facade
 HUFF_TEST   := tests/cpp/bin/test_huffman_fast
+QUANT_TEST  := tests/cpp/bin/test_quant_fast
 
-all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) $(HUFF_TEST) oracle
+all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) $(HUFF_TEST) $(QUANT_TEST) oracle
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HEADERS)
 	@mkdir -p $(BUILD)
@@ -75,3 +76,8 @@ $(FACADE_TEST): tests/cpp/test_facade.cpp $(LIBDIR)/libjpge.so $(SRC)/jpge_image
 $(HUFF_TEST): tests/cpp/test_huffman_fast.cpp $(SRC)/huffman.cpp $(SRC)/huffman.hpp
 	@mkdir -p tests/cpp/bin
 	$(CXX) $(CXXFLAGS) -o $@ $< $(SRC)/huffman.cpp
+
+# K1's quantiser fast path against the reference's two roundings (tests/test_host.py runs it)
+$(QUANT_TEST): tests/cpp/test_quant_fast.cpp $(SRC)/constants.hpp
+	@mkdir -p tests/cpp/bin
+	$(CXX) -O2 -std=c++17 -ffp-contract=off -I$(SRC) -o $@ $<

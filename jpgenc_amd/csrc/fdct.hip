@@ -35,8 +35,9 @@ constexpr double kCrR = (double).5f, kCrG = (double)-.4186f, kCrB = (double)-.08
 // away from zero.  Fast path in one fp64 instruction per coefficient: the exact
 // product x = w * c, c = fl(s_u / q), is within 2^-40 of the reference's quotient
 // fl(fl(w s_u) / q) (|x| < 2^11: 8-bit samples, q >= 1), and
-// y = fma(w, c, 1.5 * 2^36) rounds it once onto the 2^-16 grid, so the low word of y
-// is n = round(x * 2^16) (two's complement, mod 2^32).  With t = n + 0x8001:
+// y = fma(w, c, 1.5 * 2^36 + 0x8001 * 2^-16) rounds it once onto the 2^-16 grid (the
+// addend lies on the grid, and y stays in [2^36, 2^37)), so the low word of y is
+// t = n + 0x8001 with n = round(x * 2^16) (two's complement, mod 2^32):
 //   - t >> 16 (its high half) is floor(x + 1/2), the reference's integer unless x
 //     lies within 2^-15 of a half-integer — where the reference's quotient could sit
 //     on the other side of it;
@@ -44,10 +45,10 @@ constexpr double kCrR = (double).5f, kCrG = (double)-.4186f, kCrB = (double)-.08
 //     row's 8 values finds them, and such a row is redone the reference's way
 //     (quant_exact; rare, one wave-uniform branch per row).
 // Integer boundaries are harmless (a quotient on either side of k rounds to k).
-constexpr double kQuantMagic = 103079215104.0;  // 1.5 * 2^36: ulp 2^-16
+constexpr double kQuantMagic = 103079215104.50002;  // 1.5 * 2^36 + 0x8001 * 2^-16 (bits 0x4238000000008001)
+static_assert(kQuantMagic - 103079215104.0 == 0x8001 * 0x1p-16, "the magic addend is exact");
 __device__ __forceinline__ uint32_t quant_fix16(double w, double c) {
-    const double y = __builtin_fma(w, c, kQuantMagic);
-    return (uint32_t)__builtin_bit_cast(uint64_t, y) + 0x8001u;
+    return (uint32_t)__builtin_bit_cast(uint64_t, __builtin_fma(w, c, kQuantMagic));
 }
 
 __device__ __forceinline__ int quant_exact(double w, double s, double q) { return (int)round((w * s) / q); }

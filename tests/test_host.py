@@ -153,3 +153,18 @@ def test_huffman_array_emulation_matches_std_containers():
     r = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("0 mismatches")
+
+
+def test_quantiser_fast_path_matches_reference_rounding():
+    """K1's one-FMA quantiser (fdct.hip quant_fix16/quant_row) on the host: for every
+    quantiser 1..255 and column scale, random, near-half and dyadic row outputs, the
+    fast path's integer equals the reference's (int)round(fl(w*s)/q) whenever its
+    low-half test lets it stand (Coding.hpp:92-94, Dct.hpp:124-131)."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "bin", "test_quant_fast")
+    if not os.path.exists(exe):
+        pytest.skip("tests/cpp/bin/test_quant_fast not built (make)")
+    r = subprocess.run([exe, "4000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith(" 0 mismatches")
