@@ -212,12 +212,16 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
 
     // 48-byte RGB run of this lane for partition tile k, if the tile is on the aligned
     // fast path (else zeros, and the staging takes the clamped edge path)
+    // (tile numbers are wave-uniform: the tile's row and column come from scalar
+    // arithmetic, and only this lane's fixed offset within the tile is per lane)
+    const uint32_t lane_off = (uint32_t)r16 * (uint32_t)a.stride + (uint32_t)c16 * 48u;
     auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
         const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * 4;
         const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
         const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
-        const uint32_t off = ok ? (uint32_t)((uint64_t)y * a.stride + (uint64_t)xs * 3) : kOob;
+        const uint32_t base = (uint32_t)((uint64_t)(mrow * 16) * a.stride + (uint64_t)mcol0 * 48);  // (uniform)
+        const uint32_t off = ok ? base + lane_off : kOob;
         v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
         v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
         v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, K1_LOAD_AUX));
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     u32x4 pend;
     uint32_t poff = kOob;
     auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, K1_STORE_AUX); };
-    uint32_t k = wv;  // this wave's current tile of the run
+    uint32_t k = __builtin_amdgcn_readfirstlane((uint32_t)wv);  // this wave's current tile of the run
     uint4 c0, c1, c2;
     bool cfast = fast_load(k, c0, c1, c2);  // issued before the prologue's own memory traffic
 
@@ -495,12 +499,14 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
         if (lane == 0) v = atomicAdd(&lds.next, 1u);
         return __builtin_amdgcn_readfirstlane(v);
     };
+    const uint32_t lane_off = (uint32_t)r8 * (uint32_t)a.stride + (uint32_t)c8 * 48u;  // (as in fdct_kernel)
     auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
         const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * kMcus;
         const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 * kYh + c8 * 16;
         const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
-        const uint32_t off = ok ? (uint32_t)((uint64_t)y * a.stride + (uint64_t)xs * 3) : kOob;
+        const uint32_t base = (uint32_t)((uint64_t)(mrow * 8) * a.stride + (uint64_t)mcol0 * 24 * kYh);  // (uniform)
+        const uint32_t off = ok ? base + lane_off : kOob;
         v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
         v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
         v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, K1_LOAD_AUX));
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
     u32x4 pend;
     uint32_t poff = kOob;
     auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, K1_STORE_AUX); };
-    uint32_t k = wv;
+    uint32_t k = __builtin_amdgcn_readfirstlane((uint32_t)wv);
     uint4 c0, c1, c2;
     bool cfast = fast_load(k, c0, c1, c2);
 
