@@ -88,11 +88,11 @@ constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's
 #define K1_LOAD_AUX 0
 #endif
 
-// Workgroup shapes: solo, one 16-wave workgroup per CU (4 waves per SIMD), whose
-// waves balance their tiles among themselves — best when the kernel has the GPU to
-// itself (two 8-wave workgroups per CU: equal at 4K, 4% slower at 16384^2); shared,
-// 4 waves, at most two per CU, which co-schedule beside other lanes' kernels (a
-// whole-CU workgroup waits for a whole CU to drain).
+// Workgroup shapes: whole-CU, one 16-wave workgroup per CU (4 waves per SIMD), whose
+// waves balance their tiles among themselves — for large frames with the GPU to
+// itself (two 8-wave workgroups per CU: equal at 4K, 4% slower at 16384^2); 4 waves,
+// four per CU alone (smaller frames, launch_fdct) or at most two per CU beside other
+// lanes' kernels (a whole-CU workgroup waits for a whole CU to drain).
 #ifndef K1_WAVES_SOLO
 #define K1_WAVES_SOLO 16
 #endif
@@ -648,10 +648,22 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
 
 }  // namespace
 
+// Alone on the GPU, frames with fewer than kK1WholeCuTiles tiles (a 4K frame has
+// 8 100) run the 4-wave shape at 4 workgroups per CU, larger ones the whole-CU shape:
+// measured 15.5-15.6 vs 16.2-16.3 us at 4K, but 340-349 vs 317-326 us at 16384^2
+// (262 144 tiles), where the whole-CU workgroups' shared tile counter balances ~64
+// tiles per wave.
+constexpr uint32_t kK1WholeCuTiles = 65536;
+uint32_t k1_tiles(const Geometry& g) {
+    const uint32_t per = g.row8() ? 16 / g.yh : 4;  // MCUs per tile
+    return ((g.mw + per - 1) / per) * g.mh;
+}
+bool k1_whole_cu(const Geometry& g, bool solo) { return solo && k1_tiles(g) >= kK1WholeCuTiles; }
+
 template <int kYh>
 void launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
     const bool ex = a.maxval == 255;
-    if (a.solo) {
+    if (k1_whole_cu(a.g, a.solo)) {
         if (ex) (void)launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
         else (void)launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
     } else {
@@ -663,7 +675,7 @@ void launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* 
 template <int kFilt>
 void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
     const bool ex = a.maxval == 255;
-    if (a.solo) {
+    if (k1_whole_cu(a.g, a.solo)) {
         if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
         else (void)launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
     } else {
@@ -673,11 +685,15 @@ void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t
 }
 
 uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs) {
-    const uint32_t per = g.row8() ? 16 / g.yh : 4;  // MCUs per tile
-    const uint32_t tiles = ((g.mw + per - 1) / per) * g.mh;
-    // solo: one workgroup per CU (MI355X: 256 CUs); shared: four per CU, a tile per wave at a time
-    const uint32_t wgs = solo ? tiles : (tiles + kK1WavesShared - 1) / kK1WavesShared;
-    const uint32_t cap = solo ? 256u * (16u / (uint32_t)kK1WavesSolo) : override_wgs ? override_wgs : (uint32_t)K1_SHARED_CAP;
+    const uint32_t tiles = k1_tiles(g);
+    if (k1_whole_cu(g, solo)) {  // one whole-CU workgroup per CU (MI355X: 256 CUs)
+        const uint32_t cap = 256u * (16u / (uint32_t)kK1WavesSolo);
+        return tiles < cap ? tiles : cap;
+    }
+    // the 4-wave shape, a tile per wave at a time: four per CU alone, at most
+    // K1_SHARED_CAP beside other lanes
+    const uint32_t wgs = (tiles + kK1WavesShared - 1) / kK1WavesShared;
+    const uint32_t cap = override_wgs ? override_wgs : solo ? 1024u : (uint32_t)K1_SHARED_CAP;
     return wgs < cap ? wgs : cap;
 }
 
