@@ -156,10 +156,11 @@ class Encoder {
     // entropy workgroups: the override, else 512 for a single lane (its frames' latency:
     // -5 us at 4K) and seg_layout's default (384) beside other lanes (+3% throughput)
     uint32_t entropy_wgs() const { return entropy_wgs_ ? entropy_wgs_ : (lanes_.size() == 1 ? 512u : 0u); }
-    // statistics workgroups: 3 per CU alone (the shortest runs), 1 per CU beside other
-    // lanes (6 tiles per workgroup at 4K: its fixed costs, the prologue, first load and
-    // flush, amortised; 256 vs 512: +1.6% in the pipeline, 1.25, 1.5 and 0.75 per CU slower)
-    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 0u : 256u); }
+    // statistics workgroups: 2 per CU alone (4K: 29.1 us vs 30.8 at 3 per CU, 37-40 at
+    // 1.5 or 1), 1 per CU beside other lanes (6 tiles per workgroup at 4K: its fixed
+    // costs, the prologue, first load and flush, amortised; 256 vs 512: +1.6% in the
+    // pipeline, 1.25, 1.5 and 0.75 per CU slower)
+    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 512u : 256u); }
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
     // the entropy partition a slot's current frame runs on
     SegLayout slot_layout(const Slot& s) const;
