@@ -2,8 +2,11 @@
 hardware queue the kernel count and idle time, the time spent with 0/1/2/3+
 kernels running, and which kernel pairs overlap for how long.
 
-    python tools/lanes_timeline.py <dir-with-*_kernel_trace.csv> [--skip N]
+    python tools/lanes_timeline.py <dir-with-*_kernel_trace.csv> [--skip N] [--bench bench.json]
+
+--bench: only kernels inside the bench line's timed window (windows_monotonic_ns).
 """
+import json
 import argparse
 import collections
 import csv
@@ -21,13 +24,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--skip", type=int, default=400)
+    ap.add_argument("--bench")
     a = ap.parse_args()
+    win = None
+    if a.bench:
+        b = json.loads([l for l in open(a.bench) if l.startswith("{")][-1])
+        win = b["windows_monotonic_ns"]["timed"]
     ops = []
     for f in glob.glob(f"{a.dir}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"]))
     ops.sort()
-    ops = ops[a.skip:]
+    if win:
+        ops = [o for o in ops if o[0] >= win[0] and o[1] <= win[1]]
+    else:
+        ops = ops[a.skip:]
     if not ops:
         print("no operations")
         return
