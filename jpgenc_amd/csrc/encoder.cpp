@@ -471,10 +471,27 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     // lane spins for its latency.
     e->nap_ = nap < 0 ? nlanes > 1 : nap != 0;
     const int nslots = e->lookahead_ + e->drain_lag_ + 1;  // a slot is reused after its drain
+    // Several lanes: each lane's stream is created with a full CU mask, which gives it a
+    // hardware queue of its own (ROCclr hands such a stream a dedicated queue instead of
+    // one from the process's shared pool of GPU_MAX_HW_QUEUES).  From the pool, two lanes
+    // could land on one in-order queue and serialise: the 1080p batch (config 4) ran
+    // 107.8-109.9 vs 88.6-90.8 GPix/s, the same as with GPU_MAX_HW_QUEUES=6 (110.2-110.3);
+    // 4K unchanged (185.2 vs 185.4).  JPGE_CU_MASK_STREAMS=0: pool streams.
+    const bool cumask = env_int("JPGE_CU_MASK_STREAMS", nlanes > 1 ? 1 : 0, 0, 1) != 0;
+    std::vector<uint32_t> mask;
+    if (cumask) {
+        int ncu = 0;
+        JPGE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        mask.assign((size_t)(ncu + 31) / 32, 0xFFFFFFFFu);
+        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+    }
     for (int l = 0; l < nlanes; ++l) {
         std::unique_ptr<Lane> ln(new Lane());
         ln->id = l;
-        JPGE_HIP(hipStreamCreateWithFlags(&ln->stream, hipStreamNonBlocking));
+        if (cumask)
+            JPGE_HIP(hipExtStreamCreateWithCUMask(&ln->stream, (uint32_t)mask.size(), mask.data()));
+        else
+            JPGE_HIP(hipStreamCreateWithFlags(&ln->stream, hipStreamNonBlocking));
         JPGE_HIP(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
         ln->guess_hist.frac = ln->guess_result.frac = e->first_sleep_;
         for (int i = 0; i < nslots; ++i) {
