@@ -10,8 +10,10 @@ library or a GPU is missing, calls fail loudly.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -375,6 +377,21 @@ def max_jpeg_bytes(width: int, height: int) -> int:
     return int(lib().jpge_max_jpeg_bytes(width, height))
 
 
+# Encoders (and device groups) still open at interpreter exit are closed by an atexit hook, ahead of the
+# HIP runtime's own teardown in the C++ static destructors (a lane stream destroyed
+# after that, e.g. once a profiler's tool library has finalised, can fault the process).
+_live_encoders = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_encoders() -> None:
+    for e in list(_live_encoders):
+        try:
+            e.close()
+        except Exception:
+            pass
+
+
 class Encoder:
     """One GPU context (jpge_open).  Host-array methods copy in/out; the `*_dev`
     variants take device pointers (ints) for HBM-resident frames."""
@@ -383,6 +400,7 @@ class Encoder:
         """lanes: concurrent pipelines on the device (0 = JPGE_LANES or the default 4)."""
         self._ctx = ctypes.c_void_p()
         _check(lib().jpge_open_ex(int(device), int(lanes), ctypes.byref(self._ctx)), f"jpge_open({device})")
+        _live_encoders.add(self)
         self.device = device
         self._qcache = {}     # quality -> (qy, qc) byte tables
         self._desc = None     # (key, Frame array) of the last device batch
@@ -623,6 +641,7 @@ class Group:
         devs = (ctypes.c_int * len(devices))(*devices)
         self._g = ctypes.c_void_p()
         _check(lib().jpge_group_open(len(devices), devs, int(lanes), ctypes.byref(self._g)), "group_open")
+        _live_encoders.add(self)
 
     def close(self) -> None:
         if self._g:

@@ -37,3 +37,4 @@ t = enc.timing()
 f = max(1, t["frames"])
 print(f"{a.width}x{a.height} Q{a.quality} kind{a.kind}: {n[0]} bytes; fdct {t['fdct_sum']/f*1e3:.1f} us, "
       f"dc {t['dc_stats_sum']/f*1e3:.1f} us, entropy {t['entropy_sum']/f*1e3:.1f} us")
+enc.close()
