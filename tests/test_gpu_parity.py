@@ -118,6 +118,21 @@ def _encoder_with_wgs(wgs):
     return _encoder_with_env(JPGE_ENTROPY_WGS=wgs)
 
 
+# Lane streams with a hardware queue each (CU-masked, the multi-lane default) and
+# from HIP's shared pool give the same bytes; batches spread over every lane.
+@pytest.mark.parametrize("cumask", [0, 1])
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_lane_streams_bit_exact(cumask, lanes):
+    enc = _encoder_with_env(JPGE_CU_MASK_STREAMS=cumask, JPGE_LANES=lanes)
+    try:
+        frames = [J.synth_rgb8(700 + i, 256 + 32 * (i % 4), 136 + 16 * (i % 3), kind=i % 3) for i in range(12)]
+        outs = enc.encode_batch(frames, quality=90)
+        for f, o in zip(frames, outs):
+            assert o == _oracle.encode(f, 90)
+    finally:
+        enc.close()
+
+
 # The entropy kernel splits the frame's 128-block tiles into contiguous runs of
 # 2..4 tiles per workgroup; every split must give the same bytes.  Widths of
 # 65 and 129 MCUs leave a final tile of 6 blocks (a few bits).
