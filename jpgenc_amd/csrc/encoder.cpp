@@ -488,10 +488,11 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     for (int l = 0; l < nlanes; ++l) {
         std::unique_ptr<Lane> ln(new Lane());
         ln->id = l;
-        if (cumask)
-            JPGE_HIP(hipExtStreamCreateWithCUMask(&ln->stream, (uint32_t)mask.size(), mask.data()));
-        else
+        // (a runtime that refuses CU masks gets a pool stream: correct, possibly shared)
+        if (!cumask || hipExtStreamCreateWithCUMask(&ln->stream, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
             JPGE_HIP(hipStreamCreateWithFlags(&ln->stream, hipStreamNonBlocking));
+        }
         JPGE_HIP(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
         ln->guess_hist.frac = ln->guess_result.frac = e->first_sleep_;
         for (int i = 0; i < nslots; ++i) {
