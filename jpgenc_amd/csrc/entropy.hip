@@ -37,6 +37,9 @@ using namespace dev;
 // need 72 (7 waves): +0.7% over one group at 8 (2 pairs on one box; 6 waves: +0.3%)
 #define K3_WPE (K3_GROUPS > 1 ? 7 : 8)
 #endif
+#ifndef K3_ZERO128
+#define K3_ZERO128 1  // (the stage zeroed in 16-byte stores: +1-2.5% in the pipeline over 3 pairs, code kernel -0.5 us alone)
+#endif
 #ifndef K3_EMIT_MERGE
 #define K3_EMIT_MERGE 1  // a thread's 4 records written as one bit string (code kernel)
 #endif
@@ -65,7 +68,7 @@ constexpr int kRecBits = 8, kRecEdge = 9;  // u32 indices
 static_assert(sizeof(WgRecord) == kEntropyRecordBytes, "record size");
 
 struct K3Lds {
-    uint32_t stage[kStageWords];  // the tile's big-endian bit stream
+    alignas(16) uint32_t stage[kStageWords];  // the tile's big-endian bit stream
     uint32_t tab[4 * 256];        // (len << 16) | code
     uint32_t tcnt[kTcntSlots];    // symbol records of each of the workgroup's tiles
     alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
@@ -109,7 +112,12 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
+#if K3_ZERO128
+    static_assert(kStageWords % 4 == 0, "the stage zeroes in 16-byte stores");
+    for (int i = tid; i < kStageWords / 4; i += kK3Threads) reinterpret_cast<uint4*>(L.stage)[i] = make_uint4(0, 0, 0, 0);
+#else
     for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
+#endif
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
     const int ntl = (int)wt.nt;
     if (tid < ntl) L.tcnt[tid] = a.tcount[wt.seg * a.seg.tps + wt.t0 + tid];
