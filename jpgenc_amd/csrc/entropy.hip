@@ -38,7 +38,7 @@ using namespace dev;
 #define K3_WPE (K3_GROUPS > 1 ? 7 : 8)
 #endif
 #ifndef K3_ZERO128
-#define K3_ZERO128 1  // (the stage zeroed in 16-byte stores: +1-2.5% in the pipeline over 3 pairs, code kernel -0.5 us alone)
+#define K3_ZERO128 1  // (the stage zeroed in 16-byte stores; with K2's: 185.8 vs 184.4 GPix/s over 3 pairs)
 #endif
 #ifndef K3_EMIT_MERGE
 #define K3_EMIT_MERGE 1  // a thread's 4 records written as one bit string (code kernel)
@@ -68,7 +68,9 @@ constexpr int kRecBits = 8, kRecEdge = 9;  // u32 indices
 static_assert(sizeof(WgRecord) == kEntropyRecordBytes, "record size");
 
 struct K3Lds {
-    alignas(16) uint32_t stage[kStageWords];  // the tile's big-endian bit stream
+    // the tile's big-endian bit stream (offset 0 of the kernel's only __shared__ object,
+    // so 16-byte aligned; an alignas(16) here made the compiler spill 8 VGPRs)
+    uint32_t stage[kStageWords];
     uint32_t tab[4 * 256];        // (len << 16) | code
     uint32_t tcnt[kTcntSlots];    // symbol records of each of the workgroup's tiles
     alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
