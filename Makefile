@@ -81,3 +81,37 @@ $(HUFF_TEST): tests/cpp/test_huffman_fast.cpp $(SRC)/huffman.cpp $(SRC)/huffman.
 $(QUANT_TEST): tests/cpp/test_quant_fast.cpp $(SRC)/constants.hpp
 	@mkdir -p tests/cpp/bin
 	$(CXX) -O2 -std=c++17 -ffp-contract=off -I$(SRC) -o $@ $<
+
+# Host code under AddressSanitizer + UndefinedBehaviorSanitizer (run by
+# tests/test_asan.py in the CPU suite): every host .cpp of the library rebuilt
+# sanitized and linked with the (unsanitized) HIP device objects, plus the host
+# tests.  No GPU is touched: the drivers call host-only entry points.
+ASAN_FLAGS := -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer -g -O1
+ASAN_DIR   := build/asan
+ASAN_BIN   := tests/cpp/bin/asan
+ASAN_OBJS  := $(addprefix $(ASAN_DIR)/,$(HOST_SRCS:.cpp=.o))
+ASAN_TESTS := $(ASAN_BIN)/test_host_asan $(ASAN_BIN)/test_facade $(ASAN_BIN)/test_huffman_fast $(ASAN_BIN)/test_quant_fast
+
+$(ASAN_DIR)/%.o: $(SRC)/%.cpp $(HEADERS)
+	@mkdir -p $(ASAN_DIR)
+	$(CXX) $(CXXFLAGS) $(ASAN_FLAGS) -c $< -o $@
+
+$(ASAN_BIN)/test_host_asan: tests/cpp/test_host_asan.cpp $(ASAN_OBJS) $(DEV_OBJS)
+	@mkdir -p $(ASAN_BIN)
+	$(CXX) $(CXXFLAGS) $(ASAN_FLAGS) -o $@ $^ -L$(ROCM)/lib -lamdhip64 -ldl -Wl,-rpath,$(ROCM)/lib
+
+$(ASAN_BIN)/test_facade: tests/cpp/test_facade.cpp $(ASAN_OBJS) $(DEV_OBJS)
+	@mkdir -p $(ASAN_BIN)
+	$(CXX) $(CXXFLAGS) $(ASAN_FLAGS) -o $@ $^ -L$(ROCM)/lib -lamdhip64 -ldl -Wl,-rpath,$(ROCM)/lib
+
+$(ASAN_BIN)/test_huffman_fast: tests/cpp/test_huffman_fast.cpp $(SRC)/huffman.cpp $(SRC)/huffman.hpp
+	@mkdir -p $(ASAN_BIN)
+	$(CXX) $(CXXFLAGS) $(ASAN_FLAGS) -o $@ $< $(SRC)/huffman.cpp
+
+$(ASAN_BIN)/test_quant_fast: tests/cpp/test_quant_fast.cpp $(SRC)/constants.hpp
+	@mkdir -p $(ASAN_BIN)
+	$(CXX) -std=c++17 -ffp-contract=off -I$(SRC) $(ASAN_FLAGS) -o $@ $<
+
+asan: $(ASAN_TESTS)
+
+.PHONY: asan

@@ -1,9 +1,14 @@
 // extern "C" boundary (include/jpge.h) over jpge::Encoder and the host pieces.
 #include "jpge.h"
 
+#include <pthread.h>
+
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -12,6 +17,7 @@
 #include "host_io.hpp"
 #include "huffman.hpp"
 #include "ingest.hpp"
+#include "live.hpp"
 
 struct jpge_ctx {
     std::unique_ptr<jpge::Encoder> enc;
@@ -29,6 +35,78 @@ jpge::FrameDesc frame(const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride,
     return f;
 }
 }  // namespace
+
+namespace jpge {
+namespace {
+struct LiveSet {
+    std::mutex mu;
+    std::vector<jpge_ctx*> ctx;
+    std::vector<jpge_group*> grp;
+};
+LiveSet& live() {
+    static LiveSet* s = new LiveSet();  // never destroyed: it must outlive every exit handler
+    return *s;
+}
+// (live.hpp) closes every group, then every context, still open at exit
+void close_live_at_exit() {
+    for (;;) {
+        jpge_group* g = nullptr;
+        {
+            std::lock_guard<std::mutex> l(live().mu);
+            if (!live().grp.empty()) g = live().grp.back();
+        }
+        if (!g) break;
+        jpge_group_close(g);  // (removes itself and closes its member contexts)
+    }
+    for (;;) {
+        jpge_ctx* c = nullptr;
+        {
+            std::lock_guard<std::mutex> l(live().mu);
+            if (!live().ctx.empty()) c = live().ctx.back();
+        }
+        if (!c) break;
+        jpge_close(c);
+    }
+}
+void forget_in_child() {  // a forked child: the parent's lane threads do not exist here
+    live().ctx.clear();
+    live().grp.clear();
+    new (&live().mu) std::mutex();
+}
+std::once_flag g_first_open;
+template <typename T>
+void erase_one(std::vector<T*>& v, T* x) {
+    auto it = std::find(v.begin(), v.end(), x);
+    if (it != v.end()) v.erase(it);
+}
+}  // namespace
+
+void live_add(jpge_ctx* c) {
+    std::call_once(g_first_open, [] {
+        live();
+        std::atexit(close_live_at_exit);
+        pthread_atfork(nullptr, nullptr, forget_in_child);
+    });
+    std::lock_guard<std::mutex> l(live().mu);
+    live().ctx.push_back(c);
+}
+void live_remove(jpge_ctx* c) {
+    std::lock_guard<std::mutex> l(live().mu);
+    erase_one(live().ctx, c);
+}
+void live_add(jpge_group* g) {
+    std::lock_guard<std::mutex> l(live().mu);
+    live().grp.push_back(g);
+}
+void live_remove(jpge_group* g) {
+    std::lock_guard<std::mutex> l(live().mu);
+    erase_one(live().grp, g);
+}
+void live_handler_after_load() {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(close_live_at_exit); });
+}
+}  // namespace jpge
 
 extern "C" {
 
@@ -68,10 +146,12 @@ int jpge_open_ex(int device, int lanes, jpge_ctx** ctx) {
     int st = jpge::Encoder::open(device, c->enc, lanes);
     if (st) return st;
     *ctx = c.release();
+    jpge::live_add(*ctx);  // (closed at exit if the caller does not: live.hpp)
     return JPGE_OK;
 }
 
 int jpge_close(jpge_ctx* ctx) {
+    if (ctx) jpge::live_remove(ctx);
     delete ctx;
     return JPGE_OK;
 }

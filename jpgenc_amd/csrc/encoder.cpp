@@ -585,7 +585,7 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
         hipFree(s.d_recs); hipFree(s.d_tcount);
         s.d_recs = nullptr; s.d_tcount = nullptr; s.cap_tiles = s.cap_recs = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_recs, nrecs * sizeof(*s.d_recs)));
-        JPGE_HIP(hipMalloc((void**)&s.d_tcount, ntiles * 4));
+        JPGE_HIP(hipMalloc((void**)&s.d_tcount, ntiles * kRecSub * 4));
         s.cap_tiles = ntiles;
         s.cap_recs = nrecs;
     }
@@ -1017,9 +1017,6 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
                                sp->tables_done.store(1, std::memory_order_release);
                            },
                            {}});
-        } else {
-            s.tables_status = build_tables(s, true);
-            s.tables_done.store(1, std::memory_order_release);
         }
     };
     // diagnostic host trace: (iteration, point, us since the call, and at point 1 the
@@ -1068,7 +1065,8 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         if (j >= 0 && j < n && !frame(j).status) {
             Slot& s = *ln.slots[j % S];
             if (s.inline_tables && !s.tables_done.load(std::memory_order_acquire)) {
-                s.tables_status = build_tables(s, false);
+                // (no pool: a single-frame encode builds its four tables in parallel)
+                s.tables_status = build_tables(s, /*parallel=*/!pool_);
                 s.tables_done.store(1, std::memory_order_release);
             }
             while (!s.tables_done.load(std::memory_order_acquire)) {

@@ -160,7 +160,8 @@ class Encoder {
     // 1.5 or 1), 1 per CU beside other lanes (6 tiles per workgroup at 4K: its fixed
     // costs, the prologue, first load and flush, amortised; 256 vs 512: +1.6% in the
     // pipeline, 1.25, 1.5 and 0.75 per CU slower)
-    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 512u : 256u); }
+    // (statistics workgroups of 8 waves: 3 per CU alone, 1.5 per CU beside other lanes)
+    uint32_t stats_wgs() const { return stats_wgs_ ? stats_wgs_ : (lanes_.size() == 1 ? 768u : 384u); }
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
     // the entropy partition a slot's current frame runs on
     SegLayout slot_layout(const Slot& s) const;

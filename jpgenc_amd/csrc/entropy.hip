@@ -50,7 +50,7 @@ constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
 constexpr int kMaxTiles = kEntropyMaxTilesPerWg;
-constexpr int kTcntSlots = kMaxTiles;  // tiles of a workgroup
+constexpr int kTcntSlots = kMaxTiles * kRecSub;  // record sub-streams of a workgroup's tiles
 constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-case tile + lead
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
@@ -72,7 +72,7 @@ struct K3Lds {
     // so 16-byte aligned; an alignas(16) here made the compiler spill 8 VGPRs)
     uint32_t stage[kStageWords];
     uint32_t tab[4 * 256];        // (len << 16) | code
-    uint32_t tcnt[kTcntSlots];    // symbol records of each of the workgroup's tiles
+    uint32_t tcnt[kTcntSlots];    // symbol records of each sub-stream of the workgroup's tiles
     alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
     uint32_t cnt8[8];
     uint32_t carry;
@@ -121,8 +121,8 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
 #endif
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
-    const int ntl = (int)wt.nt;
-    if (tid < ntl) L.tcnt[tid] = a.tcount[wt.seg * a.seg.tps + wt.t0 + tid];
+    const int ntl = (int)wt.nt * kRecSub;  // the tiles' record sub-streams (kernels.hpp)
+    if (tid < ntl) L.tcnt[tid] = a.tcount[(wt.seg * a.seg.tps + wt.t0) * kRecSub + tid];
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
 
@@ -151,9 +151,9 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     // zeros), so no branch merges in-flight registers and the in-order wait for a
     // round's records never waits for the prefetch behind it.
     const uint32_t gt0 = wt.seg * a.seg.tps + wt.t0;  // global number of the first tile
-    constexpr uint32_t slot = kTileRecords;  // records per tile
+    constexpr uint32_t slot = kSubRecords;  // records per sub-stream
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * slot), 0, ntl * slot * 4, 0x00020000);
+        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * slot * 4, 0x00020000);
     constexpr int kGroups = K3_GROUPS;            // groups of 4 records per thread and round
     constexpr uint32_t kRound = 4 * kGroups * kK3Threads;  // records per round
     // The workgroup's records are one stream over its tiles: tile t's count padded to a

@@ -661,26 +661,26 @@ uint32_t k1_tiles(const Geometry& g) {
 bool k1_whole_cu(const Geometry& g, bool solo) { return solo && k1_tiles(g) >= kK1WholeCuTiles; }
 
 template <int kYh>
-void launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
+hipError_t launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
     const bool ex = a.maxval == 255;
     if (k1_whole_cu(a.g, a.solo)) {
-        if (ex) (void)launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
-        else (void)launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
     } else {
-        if (ex) (void)launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
-        else (void)launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
     }
 }
 
 template <int kFilt>
-void launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
+hipError_t launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
     const bool ex = a.maxval == 255;
     if (k1_whole_cu(a.g, a.solo)) {
-        if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
-        else (void)launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        else return launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
     } else {
-        if (ex) (void)launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
-        else (void)launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        else return launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
     }
 }
 
@@ -705,21 +705,20 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
     // the kernels assume these shapes (kernels.hpp Geometry)
     if (a.g.row8()) {
         switch (a.g.yh) {
-            case 1: if (a.g.bpm != 3) return hipErrorInvalidValue; launch_row8<1>(a, grid, s, t); break;
-            case 2: if (a.g.bpm != 4) return hipErrorInvalidValue; launch_row8<2>(a, grid, s, t); break;
-            case 4: if (a.g.bpm != 6) return hipErrorInvalidValue; launch_row8<4>(a, grid, s, t); break;
+            // (launch_timed returns the launch's error: hipGetLastError has already consumed it)
+            case 1: return a.g.bpm != 3 ? hipErrorInvalidValue : launch_row8<1>(a, grid, s, t);
+            case 2: return a.g.bpm != 4 ? hipErrorInvalidValue : launch_row8<2>(a, grid, s, t);
+            case 4: return a.g.bpm != 6 ? hipErrorInvalidValue : launch_row8<4>(a, grid, s, t);
             default: return hipErrorInvalidValue;
         }
-        return hipGetLastError();
     }
     if (a.g.yh != 2 || a.g.bpm != 6) return hipErrorInvalidValue;
     switch (a.g.cfilt) {
-        case kFiltS420m: launch_420<kFiltS420m>(a, grid, s, t); break;
-        case kFiltS420lm: launch_420<kFiltS420lm>(a, grid, s, t); break;
-        case kFiltS420: launch_420<kFiltS420>(a, grid, s, t); break;
+        case kFiltS420m: return launch_420<kFiltS420m>(a, grid, s, t);
+        case kFiltS420lm: return launch_420<kFiltS420lm>(a, grid, s, t);
+        case kFiltS420: return launch_420<kFiltS420>(a, grid, s, t);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 }  // namespace jpge

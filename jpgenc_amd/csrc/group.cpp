@@ -29,6 +29,7 @@
 #include <rccl/rccl.h>
 
 #include "jpge.h"
+#include "live.hpp"
 
 namespace {
 
@@ -197,12 +198,15 @@ int jpge_group_open(int ndev, const int* devices, int lanes, jpge_group** g) {
         G->comm.assign(n, nullptr);
         if (rccl().commInitAll(G->comm.data(), n, G->dev.data()) != ncclSuccess) return (int)JPGE_E_RCCL;
         G->use_rccl = true;
+        jpge::live_handler_after_load();  // (after RCCL's own initialisation: live.hpp)
     }
     *g = G.release();
+    jpge::live_add(*g);
     return (int)JPGE_OK;
 }
 
 int jpge_group_close(jpge_group* g) {
+    if (g) jpge::live_remove(g);
     delete g;
     return (int)JPGE_OK;
 }

@@ -108,7 +108,7 @@ int jpge_huffman_decode(const uint8_t* bits, uint64_t nbits, const uint32_t* tab
     // (fewer at the end, the rest 1-filled) and pick the first code, in order of the
     // 1-filled codes, that is >= them.  For a prefix code that is the code the bits
     // start with.
-    if (!bits || !table_syms || !table_codes || !table_lens || !n || nsym <= 0 || nsym > 256) return JPGE_E_ARG;
+    if (!bits || !table_syms || !table_codes || !table_lens || !n || nsym <= 0 || nsym > (1 << 15)) return JPGE_E_ARG;  // (package_merge: <= 2^15 symbols, Huffman.hpp:115)
     struct Entry { uint32_t filled; int len; int sym; };
     std::vector<Entry> e;
     int maxlen = 0;

@@ -88,6 +88,19 @@ inline int tri(int x, int period) {  // triangle wave 0..255
     return (p < h ? p : period - p) * 255 / (h ? h : 1);
 }
 
+// loadP3PPM's fast_atoi (Image.cpp:393-408): digits accumulated without validation.
+// The reference's int overflows (undefined) on long tokens; here an accumulator that
+// leaves +-2^40 stops at -1, which every caller rejects as out of range, and every
+// token that stays inside that range gets the reference's value.
+inline long fast_atoi(const std::string& wd) {
+    long v = 0;
+    for (char c : wd) {
+        v = v * 10 + (c - '0');
+        if (v > (1l << 40) || v < -(1l << 40)) return -1;
+    }
+    return v;
+}
+
 }  // namespace
 
 int parse_ppm(const uint8_t* buf, size_t n, PpmImage& out) {
@@ -112,8 +125,7 @@ int parse_ppm(const uint8_t* buf, size_t n, PpmImage& out) {
         for (size_t i = 0; i < cnt; ++i) {
             std::string wd = t.word();
             if (wd.empty() && t.pos() >= n) return kErrTruncated;
-            long v = 0;
-            for (char c : wd) v = v * 10 + (c - '0');
+            const long v = fast_atoi(wd);
             if (v < 0 || v > mv) return kErrRange;
             out.rgb[i] = (uint8_t)v;
         }
@@ -146,8 +158,7 @@ int parse_ppm_inplace(uint8_t* buf, size_t n, uint32_t& width, uint32_t& height,
     for (size_t i = 0; i < cnt; ++i) {
         std::string wd = t.word();
         if (wd.empty() && t.pos() >= n) return kErrTruncated;
-        long v = 0;
-        for (char c : wd) v = v * 10 + (c - '0');
+        const long v = fast_atoi(wd);
         if (v < 0 || v > mv) return kErrRange;
         buf[i] = (uint8_t)v;
     }

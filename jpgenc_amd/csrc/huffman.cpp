@@ -159,13 +159,25 @@ class HashOrder {
         }();
         return bc.data();
     }
+    static constexpr uint32_t kMaxBuckets = kMaxSyms + 64;
+    // order() sizes its bucket array for libstdc++'s growth policy (at most 257 buckets
+    // for 256 keys); a standard library that grows further takes the std-container path
+    static bool usable() {
+        static const bool ok = [] {
+            const uint32_t* bc = buckets();
+            for (int k = 0; k <= kMaxSyms; ++k)
+                if (bc[k] > kMaxBuckets) return false;
+            return true;
+        }();
+        return ok;
+    }
     // iteration order (indices into keys) after inserting distinct keys[0..n) (std::hash<int>:
     // the value as size_t, so a negative key hashes to 2^64 + key)
     static void order(const int* keys, int n, int* out) {
         constexpr int kNone = -1, kBefore = -2;  // bucket empty / its predecessor is before_begin
         const uint32_t* bc = buckets();
         int next[kMaxSyms];
-        int bucket[kMaxSyms + 64];  // node before the bucket's first node
+        int bucket[kMaxBuckets];  // node before the bucket's first node (usable())
         uint32_t nb = bc[0];
         int head = kNone;
         for (uint32_t b = 0; b < nb; ++b) bucket[b] = kNone;
@@ -364,7 +376,7 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
 void build_code_lengths(const std::vector<std::pair<int, int>>& first_order_counts,
                         std::vector<std::vector<int>>& by_len) {
     const int n = (int)first_order_counts.size();
-    if (n > kMaxSyms) {  // (symbol texts beyond byte symbols: the facade only)
+    if (n > kMaxSyms || !HashOrder::usable()) {  // (symbol texts beyond byte symbols: the facade only)
         build_code_lengths_std(first_order_counts, by_len);
         return;
     }
@@ -425,6 +437,7 @@ bool build_table_std(const uint32_t counts[256], const uint64_t first_key[256], 
 }
 
 bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out) {
+    if (!HashOrder::usable()) return build_table_std(counts, first_key, out);
     // symbols in first-occurrence order
     uint64_t key[kMaxSyms];
     int syms[kMaxSyms], cnts[kMaxSyms], n = 0;

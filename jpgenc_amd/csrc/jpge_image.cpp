@@ -18,8 +18,8 @@ using detail::check;
 using detail::fail;
 
 jpge_ctx* default_context() {
-    // opened once and never closed: closing it from a static destructor would run HIP
-    // calls during the runtime's own teardown
+    // opened once; never closed here (a static destructor would run HIP calls during
+    // the runtime's own teardown): the library's exit handler closes it (live.hpp)
     static jpge_ctx* ctx = nullptr;
     static int status = 0;
     static std::once_flag once;

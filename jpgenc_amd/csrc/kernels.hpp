@@ -153,6 +153,17 @@ JPGE_HD inline WgTiles wg_tiles(const SegLayout& L, uint32_t w) {
 // segment by segment.
 constexpr int kRecPerBlock = 64;
 constexpr int kTileRecords = kEntropyTile * kRecPerBlock;
+// A tile's records are written as kRecSub sub-streams, one per wave of the
+// statistics kernel: sub-stream j of a tile of nb blocks holds blocks
+// [j*nb/kRecSub, (j+1)*nb/kRecSub) of the tile, at recs + t*kTileRecords +
+// j*kSubRecords, its count at tcount[t*kRecSub + j].  The code kernel reads a
+// tile's sub-streams in order, so they form the tile's one record stream.
+#ifndef K2_SUB
+#define K2_SUB 4
+#endif
+constexpr int kRecSub = K2_SUB;
+constexpr int kSubRecords = kTileRecords / kRecSub;
+static_assert(kTileRecords % kRecSub == 0, "sub-streams divide a tile's records");
 
 struct StatsArgs {
     const int16_t* coef;
@@ -166,7 +177,7 @@ struct StatsArgs {
     uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
     SegLayout seg;       // the entropy partition: the tiles the records are written in
     uint32_t* recs;      // [tiles][kTileRecords] symbol records
-    uint32_t* tcount;    // [tiles] records per tile
+    uint32_t* tcount;    // [tiles][kRecSub] records per sub-stream
     uint32_t wgs = 0;    // workgroup count (0 = 3 per CU; the pipeline passes its own, stats_grid)
     uint64_t* dbg;
 };
@@ -249,6 +260,15 @@ JPGE_HD inline void seg_tile(const SegLayout& L, uint32_t gt, uint64_t& b0, uint
     }
     b0 = (uint64_t)seg * L.sblk + (uint64_t)i * nbs / tps;
     nb = (uint32_t)((uint64_t)(i + 1) * nbs / tps - (uint64_t)i * nbs / tps);
+}
+// record sub-stream s (tile s / kRecSub, part s % kRecSub) and its blocks
+JPGE_HD inline void sub_tile(const SegLayout& L, uint32_t s, uint64_t& b0, uint32_t& nb) {
+    uint64_t tb;
+    uint32_t tn;
+    seg_tile(L, s / kRecSub, tb, tn);
+    const uint32_t j = s % kRecSub;
+    b0 = tb + j * tn / kRecSub;
+    nb = (j + 1) * tn / kRecSub - j * tn / kRecSub;
 }
 
 inline uint32_t entropy_tiles(const Geometry& g) {

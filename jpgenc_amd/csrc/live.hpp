@@ -1,0 +1,27 @@
+// Live contexts and device groups, closed by the library at process exit.
+//
+// A context owns lane threads, HIP streams, device and pinned host memory; a group
+// also owns RCCL communicators.  Left open at exit (a C caller that skips
+// jpge_close, the facade's default context, a Python process whose objects outlive
+// its own hooks), their teardown would otherwise run inside or after the static
+// destructors of the HIP runtime, of RCCL and of a profiler's tool library, in an
+// order nobody controls (round 3: a lane stream destroyed after rocprofv3's tool had
+// finalised faulted the process).  The library therefore registers an exit handler
+// (std::atexit) the first time a context opens, and again once RCCL is loaded:
+// handlers run in reverse order of registration, so this one runs before the
+// teardown of every runtime that was initialised before it, and closes what is still
+// open: groups first (with their member contexts), then contexts.  A forked child
+// forgets the parent's objects (their threads do not exist in it).
+#pragma once
+
+struct jpge_ctx;
+struct jpge_group;
+
+namespace jpge {
+void live_add(jpge_ctx* c);
+void live_remove(jpge_ctx* c);
+void live_add(jpge_group* g);
+void live_remove(jpge_group* g);
+// register the exit handler again, after loading a runtime with its own teardown (RCCL)
+void live_handler_after_load();
+}  // namespace jpge

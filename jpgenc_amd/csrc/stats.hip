@@ -14,6 +14,7 @@
 // the symbol, see huffman.hpp) are kept workgroup-relative in u32 LDS words and
 // widened at the flush; the global key is stored inverted so atomicMax keeps the
 // minimum.
+#include <algorithm>
 #include <cstddef>
 
 #include "device_common.hpp"
@@ -22,6 +23,12 @@ namespace jpge {
 namespace {
 using namespace dev;
 
+#ifndef K2_WAVE
+#define K2_WAVE 1  // stats_wave_kernel (one wave per block, lane = zig-zag position); 0: the round-3 kernel
+#endif
+static_assert(K2_WAVE ? kRecSub > 1 : kRecSub == 1, "the round-3 kernel writes whole-tile record streams (K2_SUB=1)");
+
+#if !K2_WAVE
 #ifndef K2_STEP
 #define K2_STEP 128
 #endif
@@ -416,6 +423,354 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
     __syncthreads();
     JPGE_STAMP(3);
 }
+#endif  // !K2_WAVE
+
+#if K2_WAVE
+// ---------------------------------------------------------------------------
+// stats_wave_kernel: one wavefront per block at a time, lane p = zig-zag position p.
+//
+// A workgroup owns a contiguous run of record sub-streams (kernels.hpp: a quarter
+// of an entropy tile, <= 32 blocks); its waves take them one at a time from an LDS
+// counter and code each alone: no workgroup barrier between the prologue and the
+// flush.  Per sub-stream a wave stages the blocks (natural order; the next
+// sub-stream it takes is loaded into registers meanwhile) in its own LDS area,
+// derives the per-block fields lane-parallel (lane j = block j: MCU, slot, text
+// index, the DC difference to the chain predecessor, the DC record), then walks the
+// blocks two at a time (their dependent chains interleave):
+//   c    = the coefficient at zig-zag position p (one ds_read_i16 per lane)
+//   M    = ballot(c != 0) without the DC: the block's AC non-zero mask, in SGPRs
+//   rank = mbcnt(M): the record index of every non-zero (DC first, then AC in order)
+//   run  = clz of M's bits below p: the zeros since the previous non-zero
+//   cat  = frexp exponent of (float)c = bit length of |c| (getCategoryAndCode)
+// and stores the block's records with one buffer store (consecutive addresses: the
+// non-zeros, and lane 63 as the EOB when coefficient 63 is zero; lanes without a
+// record store out of range, which the hardware drops).  Histogram counters are LDS
+// atomics on the workgroup's copies (lane & 1: same-symbol lanes of one instruction
+// land on different copies and banks), first-occurrence keys a read and a rare
+// atomicMin; lanes without a record touch a dummy word of their own, so none of it
+// needs an exec mask.  A block with a run of 16+ zeros before a non-zero (rare)
+// takes a wave scan for its ZRL records.  The DC records of a sub-stream are stored
+// together after its blocks, lane j at block j's first record.
+// Reference: DC chain Image.cpp:638-678, RLE + category Coding.hpp:148-283 and
+// Image.cpp:680-735, texts Image.cpp:888-906.
+#ifndef K2W_WAVES
+#define K2W_WAVES 8  // (8-wave workgroups: 28.9 us alone at 4K vs 39.7 with 4; 16 waves: 148 GPix/s in the pipeline)
+#endif
+#ifndef K2W_COPIES
+#define K2W_COPIES 8
+#endif
+#ifndef K2W_DUMMY_ADD
+#define K2W_DUMMY_ADD 0  // 1: lanes without a record add into a dummy word of their own instead of being masked off
+#endif
+constexpr int kWWaves = K2W_WAVES;
+constexpr int kWThreads = 64 * kWWaves;
+constexpr int kSubBlocks = (kEntropyTile + kRecSub - 1) / kRecSub;  // blocks of a sub-stream, at most
+static_assert(kRecSub > 1 && kSubBlocks <= 64 && kSubBlocks % 8 == 0, "a sub-stream's blocks fit a wave");
+constexpr int kWRows = kSubBlocks * 8 / 64;  // 16-byte block rows per lane = 8-block chunks per sub-stream
+constexpr int kWCopies = K2W_COPIES;
+// Counter / key words: table t's symbol s at kTabBase(t) + (s & 15) + 19 * (s >> 4).
+// The stride 19 puts the frequent symbols (runs 0-4, sizes 1-5) on distinct banks
+// (a stride of 16 put runs 0 and 2, or 1 and 3, of a size on one bank), and is
+// injective for sizes up to 18.
+constexpr uint32_t kRunStride = 19;
+constexpr uint32_t kAcWords = 15 + kRunStride * 15 + 1;  // 301
+__host__ __device__ constexpr uint32_t tab_base(uint32_t t) { return (t >> 1) * (16 + kAcWords) + (t & 1) * 16; }
+constexpr uint32_t kWSyms = tab_base(3) + kAcWords;  // 634 words: Y-DC, Y-AC, C-DC, C-AC
+constexpr uint32_t kWDummy = kWSyms;                  // + lane: the words of lanes without a record
+// copy stride == 32 / copies (mod 32): the copies of a word sit on distinct banks
+constexpr uint32_t kWBankStep = 32u / kWCopies;
+constexpr uint32_t kWCopyWords = (kWSyms + 64 + 31 - kWBankStep) / 32 * 32 + kWBankStep;
+static_assert(kWCopies <= 32 && kWCopyWords % 32 == kWBankStep && kWCopyWords >= kWSyms + 64, "copy stride");
+constexpr uint32_t kWKeyWords = (kWSyms + 1 + 3) / 4 * 4;  // keys, then one shared dummy word
+constexpr uint32_t kWMaxSubs = 1024;  // sub-streams per workgroup, at most (stats_grid)
+
+// v[lane] = x: v_writelane with the lane select in M0 (gfx950 reads one scalar
+// operand per VALU instruction besides M0), one VALU instead of a compare and a
+// select.  M0 is the compiler's: saved and restored around the write.
+__device__ __forceinline__ void set_lane(uint32_t& v, uint32_t x, uint32_t lane) {
+    uint32_t sv;
+    asm volatile("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
+                 : "+v"(v), "=&s"(sv)
+                 : "s"(x), "s"(lane));
+}
+
+// zig-zag position -> natural index (inverse of Coding.hpp:57-81)
+static __constant__ uint8_t kZzToNat[64] = {
+    0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+struct K2WLds {
+    alignas(16) uint32_t stage[kWWaves][8 * 32];        // each wave's 8-block chunk: int16 [block][64], natural order
+    alignas(16) uint32_t cnt[kWCopies * kWCopyWords];    // counters [copy][word], then the dummies
+    alignas(16) uint32_t key[kWKeyWords];                // first-occurrence keys (min), workgroup-relative
+    uint32_t sb0[kWMaxSubs + 1];                         // the workgroup's sub-streams' first blocks, and the end
+    uint32_t next;                                       // the next sub-stream to take
+};
+
+__global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
+    __shared__ K2WLds L;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    static_assert((kWCopies * kWCopyWords) % 4 == 0 && kWKeyWords % 4 == 0, "16-byte initialisation");
+    for (int i = tid; i < (int)(kWCopies * kWCopyWords / 4); i += kWThreads)
+        reinterpret_cast<uint4*>(L.cnt)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < (int)(kWKeyWords / 4); i += kWThreads)
+        reinterpret_cast<uint4*>(L.key)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+
+    const uint32_t bpm = a.g.bpm, mw = a.g.mw, yh = a.g.yh, yv = a.g.yv();
+    const uint32_t yhs = (uint32_t)__builtin_ctz(yh);
+    const uint32_t ybw = mw * yh;  // Y blocks per block row
+    const uint32_t S = seg_tiles(a.seg) * kRecSub;
+    // the workgroup's sub-streams [s_lo, s_hi) (64-bit divisions lane-parallel, on the VALU)
+    uint32_t s_lo, s_hi;
+    {
+        const uint32_t w = blockIdx.x + (uint32_t)(lane & 1);
+        const uint32_t v = (uint32_t)((uint64_t)w * S / gridDim.x);
+        s_lo = __builtin_amdgcn_readlane(v, 0);
+        s_hi = __builtin_amdgcn_readlane(v, 1);
+    }
+    const uint32_t ns = s_hi - s_lo;  // (<= kWMaxSubs: stats_grid)
+    for (uint32_t i = tid; i <= ns; i += kWThreads) {  // their first blocks (block numbers < 2^32: launch_stats)
+        uint64_t b;
+        uint32_t n;
+        sub_tile(a.seg, min(s_lo + i, S - 1), b, n);
+        L.sb0[i] = (uint32_t)(s_lo + i < S ? b : b + n);
+    }
+    if (tid == 0) L.next = kWWaves;  // (sub-stream w is wave w's first)
+    __syncthreads();
+    if (ns == 0) return;
+    // key bases (keys are kept relative to them): the workgroup's first MCU row
+    const uint32_t mrow0 = __builtin_amdgcn_readfirstlane((L.sb0[0] / bpm) / mw);
+    const uint32_t ybase = mrow0 * yv * ybw, cbase = mrow0 * mw;
+    JPGE_STAMP(0);
+    uint64_t tq = JPGE_NOW();
+
+    const uint32_t natoff = kZzToNat[lane];  // this lane's coefficient in a staged block (int16 index)
+    const uint32_t k2p = 2u * (uint32_t)lane;
+    uint32_t* const cnt = L.cnt + (uint32_t)(lane & (kWCopies - 1)) * kWCopyWords;
+    const uint32_t dummy = kWDummy + (uint32_t)lane;  // this lane's dummy counter word
+    const uint32_t shl = (uint32_t)(64 - lane) & 63u;
+    const uint64_t lanes_ac = ~1ull;  // every lane but the DC
+    int16_t* st16 = reinterpret_cast<int16_t*>(L.stage[wv]);
+    uint4* st4 = reinterpret_cast<uint4*>(L.stage[wv]);
+
+    uint4 cur[kWRows];
+    int dcs = 0;  // lane l < nb + 6: the DC of block b0 - 6 + l of the fetched sub-stream (0 before the frame)
+    auto rows = [&](uint32_t si) {  // sub-stream si's coefficients through a buffer descriptor (zeros past its blocks)
+        const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(a.coef + (uint64_t)b0 * 64), 0, nb * 128,
+                                                 0x00020000);
+    };
+    auto load_row = [&](const __amdgpu_buffer_rsrc_t& rs, int i) {
+        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + 64 * i) * 16, 0, 0));
+    };
+    auto load_dcs = [&](uint32_t si) {
+        const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
+        const int64_t g = (int64_t)b0 - 6 + lane;
+        dcs = ((uint32_t)lane < nb + 6 && g >= 0) ? a.coef[(uint64_t)g * 64] : 0;
+    };
+    uint32_t si = (uint32_t)wv;
+    if (si < ns) {
+        const __amdgpu_buffer_rsrc_t rs = rows(si);
+#pragma unroll
+        for (int i = 0; i < kWRows; ++i) cur[i] = load_row(rs, i);
+        load_dcs(si);
+    }
+    while (si < ns) {
+        const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
+        const uint32_t s = s_lo + si;
+        // take the next sub-stream (its rows load chunk by chunk, as this one's are staged)
+        uint32_t sn = 0;
+        if (lane == 0) sn = atomicAdd(&L.next, 1u);
+        sn = __builtin_amdgcn_readfirstlane(sn);
+        const __amdgpu_buffer_rsrc_t rsn = rows(sn < ns ? sn : si);
+
+        // ---- per block fields, lane j = block j ----
+        const uint32_t g = b0 + (uint32_t)lane;
+        const uint32_t m6 = g / bpm, k = g - m6 * bpm;
+        const uint32_t mrow = m6 / mw, mcol = m6 - mrow * mw;
+        const int comp = block_comp((int)k, bpm);
+        // text index (the Y text in block raster order; all Cr after all Cb), relative to the bases
+        const uint32_t rel = comp == 0 ? (mrow * yv + (k >> yhs)) * ybw + mcol * yh + (k & (yh - 1)) - ybase
+                                       : (m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
+        const uint32_t tsel = comp != 0;
+        // AC key base (text index * 128; a key is base + 2p + 1), its bit 0 = tsel: the
+        // block loop reads one word per block
+        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7) | tsel;
+        // DC difference to the chain predecessor: the previous Y slot, 3 blocks back for an
+        // MCU's first Y block, bpm back for chroma; none in the first MCU; restarts reset it
+        int dd;
+        {
+            const bool ynext = k >= 1 && k < bpm - 2;
+            const int back = ynext ? 1 : (k == 0 ? 3 : (int)bpm);
+            const bool none = !ynext && g < bpm;
+            bool reset = false;
+            if (a.rst.mcus && (k == 0 || k >= bpm - 2)) reset = (m6 + a.rst.mcu0) % a.rst.mcus == 0;
+            const int dcv = __builtin_amdgcn_ds_bpermute((lane + 6) * 4, dcs);
+            int pd = __builtin_amdgcn_ds_bpermute((lane + 6 - back) * 4, dcs);  // (lane - back >= -6)
+            pd = reset ? 0 : none ? (comp == 0 ? a.seed.v[0] : comp == 1 ? a.seed.v[1] : a.seed.v[2]) : pd;
+            dd = (int)(int16_t)dcv - (int)(int16_t)pd;
+        }
+        if (sn < ns) load_dcs(sn);
+        const int dcat = __builtin_amdgcn_frexp_expf((float)dd);
+        const uint32_t drec = rec_word(2u * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
+        JPGE_ACC(1, tq);
+
+        // ---- the blocks ----
+        uint32_t* srec = a.recs + (uint64_t)(s / kRecSub) * kTileRecords + (s % kRecSub) * kSubRecords;
+        const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(srec, 0, kSubRecords * 4, 0x00020000);
+        uint32_t base = 0;   // the block's first record (its DC) in the sub-stream
+        uint32_t bvec = 0;   // lane j: block j's first record
+        // one block's fields (lane p: zig-zag position p)
+        struct Blk {
+            uint64_t M, em;     // AC non-zeros; the lanes with a record (+ lane 63: non-zero, or the EOB)
+            uint32_t rk, run;   // record index in the block (DC = 0), zeros before the coefficient
+            uint32_t rec, w;    // the record; its counter / key word
+            uint32_t Tj, acbj, acw;  // the block's AC table (top byte), key base, table base word
+            bool zrl;           // a run of 16+ zeros before a non-zero
+        };
+        auto prep = [&](int c, uint32_t jb) {
+            Blk b;
+            b.M = __ballot(c != 0) & lanes_ac;
+            const uint32_t ab = __builtin_amdgcn_readlane(acb, jb);
+            b.Tj = (ab & 1u) ? 3u << 24 : 1u << 24;  // the AC table, as a record's top byte
+            b.acbj = ab | 1u;                        // (+ 2p: the key; the EOB lane 63: text * 128 + 127)
+            b.acw = (ab & 1u) ? tab_base(3) : tab_base(1);
+            b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(b.M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b.M, 1u));
+            b.run = (uint32_t)__builtin_clzll((b.M | 1ull) << shl);  // (lane 0: unused)
+            const int cat = __builtin_amdgcn_frexp_expf((float)c);
+            const uint32_t bits = extra_bits(c, cat);
+            const uint32_t rr = c != 0 ? (b.run & 15u) : 0u;  // (the EOB lane: 0)
+            b.rec = b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits;
+            b.w = b.acw + (uint32_t)cat + kRunStride * rr;
+            b.em = b.M | (1ull << 63);
+            b.zrl = (__ballot(b.run >= 16u) & b.M) != 0;
+            return b;
+        };
+        // (general form, every block with ZRLs) its records from `base`, histogram and
+        // keys; returns its record count
+        auto emit = [&](Blk b, uint32_t base) -> uint32_t {
+            uint32_t zt = 0;
+            if (b.zrl) {  // ZRL records (F/0) before the non-zeros after 16+ zeros (rare)
+                const uint32_t nzr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? b.run >> 4 : 0u;
+                const uint32_t zi = wave_scan_incl(nzr);
+                zt = __builtin_amdgcn_readlane(zi, 63);
+                b.rk += zi;
+                if (nzr) {
+                    const uint32_t zrec = b.Tj | (0xF0u << 16);
+                    for (uint32_t z = 1; z <= nzr; ++z) srec[base + b.rk - z] = zrec;
+                    const uint32_t wz = b.acw + kRunStride * 15u;  // (symbol 0xF0)
+                    atomicAdd(&cnt[wz], nzr);
+                    const uint32_t kz = b.acbj + k2p - 1u;
+                    if (kz < L.key[wz]) atomicMin(&L.key[wz], kz);
+                }
+            }
+            if (__builtin_amdgcn_inverse_ballot_w64(b.em)) {
+                srec[base + b.rk] = b.rec;
+                atomicAdd(&cnt[b.w], 1u);
+                const uint32_t kk = b.acbj + k2p;
+                if (kk < L.key[b.w]) atomicMin(&L.key[b.w], kk);
+            }
+            return 1u + (uint32_t)__builtin_popcountll(b.em) + zt;  // DC, the non-zeros and the EOB, the ZRLs
+        };
+#pragma unroll
+        for (int ch = 0; ch < kWRows; ++ch) {  // 8-block chunks: stage one, load the next sub-stream's into its registers
+            const uint32_t j0 = 8u * ch;
+            wave_order();
+            if (j0 < nb) st4[lane] = cur[ch];
+            cur[ch] = load_row(rsn, ch);
+            wave_order();
+            if (j0 >= nb) continue;
+            const uint32_t j1 = min(nb, j0 + 8u);
+            int cnA = st16[natoff], cnB = st16[64 + natoff];
+            uint32_t jb = j0;
+            for (; jb + 1 < j1; jb += 2) {
+                const int cA = cnA, cB = cnB;
+                cnA = st16[((jb + 2) & 7) * 64 + natoff];
+                cnB = st16[((jb + 3) & 7) * 64 + natoff];
+                const Blk A = prep(cA, jb), B = prep(cB, jb + 1);
+                uint32_t baseB;
+                if (!(A.zrl || B.zrl)) {
+                    // lanes without a record store out of range (dropped) and read a shared
+                    // dummy key word; their counter adds go to a dummy word of their own
+                    // (K2W_DUMMY_ADD) or are masked off
+                    baseB = base + 1u + (uint32_t)__builtin_popcountll(A.em);
+                    const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
+                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
+#if K2W_DUMMY_ADD
+                    atomicAdd(&cnt[ia ? A.w : dummy], 1u);
+                    atomicAdd(&cnt[ib ? B.w : dummy], 1u);
+#else
+                    if (ia) atomicAdd(&cnt[A.w], 1u);
+                    if (ib) atomicAdd(&cnt[B.w], 1u);
+#endif
+                    const uint32_t kwA = ia ? A.w : kWSyms, kwB = ib ? B.w : kWSyms;
+                    const uint32_t kvA = L.key[kwA], kvB = L.key[kwB];
+                    const uint32_t kkA = ia ? A.acbj + k2p : ~0u, kkB = ib ? B.acbj + k2p : ~0u;
+                    if (__ballot(kkA < kvA || kkB < kvB)) {  // (rare: a first occurrence in this workgroup so far)
+                        if (kkA < kvA) atomicMin(&L.key[kwA], kkA);
+                        if (kkB < kvB) atomicMin(&L.key[kwB], kkB);
+                    }
+                    set_lane(bvec, base, jb);
+                    set_lane(bvec, baseB, jb + 1);
+                    base = baseB + 1u + (uint32_t)__builtin_popcountll(B.em);
+                } else {
+                    set_lane(bvec, base, jb);
+                    baseB = base + emit(A, base);
+                    set_lane(bvec, baseB, jb + 1);
+                    base = baseB + emit(B, baseB);
+                }
+            }
+            if (jb < j1) {  // an odd last block
+                set_lane(bvec, base, jb);
+                base += emit(prep(cnA, jb), base);
+            }
+        }
+        JPGE_ACC(2, tq);
+        if ((uint32_t)lane < nb) {  // the DC records
+            srec[bvec] = drec;
+            const uint32_t w = tab_base(2u * tsel) + (uint32_t)dcat;
+            atomicAdd(&cnt[w], 1u);
+            if (rel < L.key[w]) atomicMin(&L.key[w], rel);
+        }
+        if (lane == 0) a.tcount[s] = base;
+        si = sn;
+        JPGE_ACC(3, tq);
+    }
+    JPGE_STAMP(2);
+    __syncthreads();
+#ifdef K2W_FLUSH  // (ablation builds only: 0 no flush, 1 counts only; outputs invalid)
+    if (K2W_FLUSH == 0) return;
+#endif
+
+    const int rep = blockIdx.x % kHistReplicas;
+    const uint64_t ncb = a.key_ncb ? a.key_ncb : a.g.nmcu();  // Cb blocks of the whole image
+    for (int i = tid; i < 1024; i += kWThreads) {
+        const uint32_t t = (uint32_t)i >> 8, sy = (uint32_t)i & 255u;
+        if (!(t & 1) && sy >= 16) continue;  // (DC tables: categories < 16)
+        const uint32_t w = tab_base(t) + (sy & 15u) + kRunStride * (sy >> 4);
+        uint32_t c = 0;
+#pragma unroll
+        for (int cp = 0; cp < kWCopies; ++cp) c += L.cnt[cp * kWCopyWords + w];
+        if (!c) continue;
+        atomicAdd(&a.hist.cnt[rep * 1024 + i], c);
+#ifdef K2W_FLUSH
+        if (K2W_FLUSH == 1) continue;
+#endif
+        const uint32_t k32 = L.key[w];
+        uint64_t kb;  // (global texts: a stripe's bases are offset into the whole image)
+        if (t < 2) kb = a.key_y0 + ybase;
+        else kb = a.key_c0 + cbase + ((k32 & 0x80000000u) ? ncb : 0ull);
+        const uint64_t gkey = ((t & 1) ? kb * 128ull : kb) + (k32 & 0x7FFFFFFFu);
+        const unsigned long long inv = ~gkey;
+        unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[i]);
+        if (inv > *gk) atomicMax(gk, inv);
+    }
+    JPGE_STAMP(3);
+}
+#endif  // K2_WAVE
 
 // Histogram export: one workgroup sums the replicas and writes the four final
 // histograms and first-occurrence keys straight into mapped host memory, then the
@@ -437,6 +792,23 @@ hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* h
     return hipGetLastError();
 }
 
+#if K2_WAVE
+uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
+    // workgroups of kWWaves waves over the record sub-streams: at least one sub-stream
+    // per wave, at most kWMaxSubs per workgroup (its LDS table)
+    const uint32_t subs = seg_tiles(L) * kRecSub;
+    const uint32_t want = wgs ? wgs : 512u;
+    const uint32_t cap = (subs + kWWaves - 1) / kWWaves;
+    const uint32_t need = (subs + kWMaxSubs - 1) / kWMaxSubs;
+    return std::max(std::max(1u, need), std::min(want, cap));
+}
+
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
+    // (32-bit block numbers and buffer offsets)
+    if ((uint64_t)a.g.nblocks() * 128 >= (1ull << 32)) return hipErrorInvalidValue;
+    return launch_timed(t, stats_wave_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kWThreads), s, a);
+}
+#else
 uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     const uint32_t tiles = seg_tiles(L);
     // persistent over contiguous runs of at most kK2MaxRun tiles: kK2PerCu per CU by
@@ -455,5 +827,6 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
     return launch_timed(t, stats_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kK2Threads), s, a);
 }
+#endif
 
 }  // namespace jpge

@@ -10,12 +10,12 @@ SLOTS = 16
 KERNELS = ["fdct", "stats", "entropy_code", "entropy_pack"]
 PHASES = {
     "fdct": ["start", "", "", "", "", "", "", "end"],
-    "stats": ["start", "", "tiles", "flush", "", "", "", ""],
+    "stats": ["start", "data", "tiles", "flush", "", "", "", ""],  # (wave kernel: wave 0's first data)
     "entropy_code": ["start", "emit", "count8", "", "", "", "", ""],
     "entropy_pack": ["start", "scan", "output", "", "", "", "", ""],
 }
 ACC = {
-    "stats": ["A masks", "B counts+scan", "C file", "D symbols"],
+    "stats": ["stage+fetch", "fields", "blocks", "DC recs"],  # (wave kernel: wave 0)
     "entropy_code": ["sync", "rounds(tail)", "store", "load+bits", "scan", "zero", "pack"],
 }
 
