@@ -535,9 +535,10 @@ def out_capacity(J, w: int, h: int) -> int:
 
 def run_batch1080(args, rank, local, world, pg):
     """Config 4: a batch of B (256) distinct 1920x1080 Q90 frames per step, frame i
-    encoded by rank i mod N; every rank's .jpg segments are gathered to rank 0 over
-    RCCL (one grouped send/recv round) inside the step, so after each step rank 0
-    holds the whole batch's files.  Strong scaling (the batch is fixed)."""
+    encoded by rank i mod N; every rank's .jpg bytes go to rank 0 packed in one RCCL
+    message per rank (jpgenc_amd/gather.py), posted at the end of the step and moving
+    while the next step encodes; the timed region ends once the last batch is on
+    rank 0.  Strong scaling (the batch is fixed)."""
     import torch
 
     import jpgenc_amd as J
@@ -554,40 +555,23 @@ def run_batch1080(args, rank, local, world, pg):
     frames = [(ins[i].data_ptr(), W, H, W * 3) for i in share]
     outd = [(outbuf.data_ptr() + k * cap, cap) for k in range(len(share))]
     enc = J.Encoder(local, lanes=args.lanes)
-    rccl = None
+    gather = None
     if world > 1:
         import torch.distributed as dist
 
+        from jpgenc_amd.gather import BatchGather
+
         rccl = gather_group(world)
         xdev = dev if dist.get_backend(rccl) == "nccl" else "cpu"  # (gloo: ranks sharing one GPU)
-        nmax = len(batch_share(B, 0, world))
-        lens_all = [torch.zeros(nmax, dtype=torch.int64, device=xdev) for _ in range(world)]
-        gather = torch.empty(B * cap if rank == 0 else 1, dtype=torch.uint8, device=xdev)
+        gather = BatchGather(rccl, dist.new_group(backend="gloo"), rank, world, B, len(share) * cap, xdev)
+        segs = [outbuf[k * cap:(k + 1) * cap] for k in range(len(share))]
 
     def step():
+        # encode this rank's share; then pack its .jpg bytes and post them to rank 0 as
+        # one message, which moves while the next step encodes (jpgenc_amd/gather.py)
         lens = enc.encode_batch_dev(frames, outd, quality=args.quality)
-        if rccl is None:
-            return lens
-        import torch.distributed as dist
-
-        mine = torch.zeros(nmax, dtype=torch.int64, device=xdev)
-        mine[:len(lens)] = torch.tensor(lens, dtype=torch.int64)
-        dist.all_gather(lens_all, mine, group=rccl)
-        src = outbuf if xdev == dev else outbuf.cpu()
-        ops = []
-        if rank == 0:
-            table = torch.stack(lens_all).cpu().tolist()
-            for r in range(1, world):
-                for k, i in enumerate(batch_share(B, r, world)):
-                    n = int(table[r][k])
-                    ops.append(dist.P2POp(dist.irecv, gather[i * cap:i * cap + n], dist.get_global_rank(rccl, r),
-                                          group=rccl))
-        else:
-            for k, n in enumerate(lens):
-                ops.append(dist.P2POp(dist.isend, src[k * cap:k * cap + n], dist.get_global_rank(rccl, 0),
-                                      group=rccl))
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
+        if gather is not None:
+            gather.post(segs if xdev == dev else [outbuf[k * cap:k * cap + n].cpu() for k, n in enumerate(lens)], lens)
         return lens
 
     for _ in range(args.warmup):
@@ -599,6 +583,8 @@ def run_batch1080(args, rank, local, world, pg):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         lens = step()
+    if gather is not None:
+        gather.wait()
     torch.cuda.synchronize()
     barrier(pg)
     dt = time.perf_counter() - t0
@@ -617,7 +603,7 @@ def run_batch1080(args, rank, local, world, pg):
                     k = share.index(i)
                     got = outbuf[k * cap:k * cap + lens[k]]
                 else:
-                    got = gather[i * cap:i * cap + len(ref)].to(dev)
+                    got = gather.frame(i).to(dev)
                 if not torch.equal(got, torch.frombuffer(bytearray(ref), dtype=torch.uint8).to(dev)):
                     bad += 1
         bad = int(sum_over_ranks(pg, float(bad)))
@@ -629,8 +615,8 @@ def run_batch1080(args, rank, local, world, pg):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 photo-like frames, seeds 1000+i, HBM-resident)",
             "config": {"workload": f"config 4: {B} x {W}x{H} 4:2:0 Q{args.quality} per step, frame i on rank i mod "
-                                   f"{world}" + (", .jpg segments gathered to rank 0 over RCCL (grouped send/recv)"
-                                                 if world > 1 else ""),
+                                   f"{world}" + (", each rank's .jpg bytes packed and sent to rank 0 as one RCCL "
+                                                 "message, overlapped with the next step's encode" if world > 1 else ""),
                        "batch": B, "width": W, "height": H, "quality": args.quality,
                        "avg_jpeg_bytes": int(nbytes / B), "parallelism": f"frames dealt over {world} GPU(s)"},
             "verified": None if args.no_verify else {

@@ -459,6 +459,9 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
 #ifndef K2W_COPIES
 #define K2W_COPIES 8
 #endif
+#ifndef K2W_WPE
+#define K2W_WPE 7  // waves per SIMD the register allocation targets (8: <= 64 VGPRs, 2 spilled; equal speed)
+#endif
 #ifndef K2W_DUMMY_ADD
 #define K2W_DUMMY_ADD 0  // 1: lanes without a record add into a dummy word of their own instead of being masked off
 #endif
@@ -486,12 +489,10 @@ constexpr uint32_t kWMaxSubs = 1024;  // sub-streams per workgroup, at most (sta
 
 // v[lane] = x: v_writelane with the lane select in M0 (gfx950 reads one scalar
 // operand per VALU instruction besides M0), one VALU instead of a compare and a
-// select.  M0 is the compiler's: saved and restored around the write.
+// select.  The statistics kernel does not use M0 otherwise (no LDS DMA, no
+// messages; checked in its ISA), so M0 is not saved around the write.
 __device__ __forceinline__ void set_lane(uint32_t& v, uint32_t x, uint32_t lane) {
-    uint32_t sv;
-    asm volatile("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
-                 : "+v"(v), "=&s"(sv)
-                 : "s"(x), "s"(lane));
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(lane));
 }
 
 // zig-zag position -> natural index (inverse of Coding.hpp:57-81)
@@ -508,7 +509,7 @@ struct K2WLds {
     uint32_t next;                                       // the next sub-stream to take
 };
 
-__global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
+__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_WPE))) void stats_wave_kernel(StatsArgs a) {
     __shared__ K2WLds L;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -595,9 +596,10 @@ __global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
         const uint32_t rel = comp == 0 ? (mrow * yv + (k >> yhs)) * ybw + mcol * yh + (k & (yh - 1)) - ybase
                                        : (m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
         const uint32_t tsel = comp != 0;
-        // AC key base (text index * 128; a key is base + 2p + 1), its bit 0 = tsel: the
-        // block loop reads one word per block
-        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7) | tsel;
+        // the block loop reads two words per block: the AC key base (text index * 128 + 1;
+        // a key is base + 2p), and the AC table as a record's top byte | its first counter word
+        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7) | 1u;
+        const uint32_t tw = ((2u * tsel + 1u) << 24) | tab_base(2u * tsel + 1u);
         // DC difference to the chain predecessor: the previous Y slot, 3 blocks back for an
         // MCU's first Y block, bpm back for chroma; none in the first MCU; restarts reset it
         int dd;
@@ -615,6 +617,7 @@ __global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
         if (sn < ns) load_dcs(sn);
         const int dcat = __builtin_amdgcn_frexp_expf((float)dd);
         const uint32_t drec = rec_word(2u * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
+        if (si == (uint32_t)wv) JPGE_STAMP(1);  // (wave 0: its first sub-stream's data is in)
         JPGE_ACC(1, tq);
 
         // ---- the blocks ----
@@ -632,13 +635,14 @@ __global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
         };
         auto prep = [&](int c, uint32_t jb) {
             Blk b;
-            b.M = __ballot(c != 0) & lanes_ac;
-            const uint32_t ab = __builtin_amdgcn_readlane(acb, jb);
-            b.Tj = (ab & 1u) ? 3u << 24 : 1u << 24;  // the AC table, as a record's top byte
-            b.acbj = ab | 1u;                        // (+ 2p: the key; the EOB lane 63: text * 128 + 127)
-            b.acw = (ab & 1u) ? tab_base(3) : tab_base(1);
-            b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(b.M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b.M, 1u));
-            b.run = (uint32_t)__builtin_clzll((b.M | 1ull) << shl);  // (lane 0: unused)
+            const uint64_t B1 = __ballot(c != 0) | 1ull;  // the AC non-zeros, and bit 0
+            b.M = B1 & lanes_ac;
+            const uint32_t twj = __builtin_amdgcn_readlane(tw, jb);
+            b.Tj = twj & 0xFF000000u;                       // the AC table, as a record's top byte
+            b.acw = twj & 0xFFFFu;                          // its first counter / key word
+            b.acbj = __builtin_amdgcn_readlane(acb, jb);    // (+ 2p: the key; the EOB lane 63: text * 128 + 127)
+            b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0u));
+            b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
             const int cat = __builtin_amdgcn_frexp_expf((float)c);
             const uint32_t bits = extra_bits(c, cat);
             const uint32_t rr = c != 0 ? (b.run & 15u) : 0u;  // (the EOB lane: 0)
@@ -683,12 +687,14 @@ __global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
             wave_order();
             if (j0 >= nb) continue;
             const uint32_t j1 = min(nb, j0 + 8u);
-            int cnA = st16[natoff], cnB = st16[64 + natoff];
+            const int16_t* cp = st16 + natoff;  // (the pair after the chunk's last reads past it: unused)
+            int cnA = cp[0], cnB = cp[64];
             uint32_t jb = j0;
             for (; jb + 1 < j1; jb += 2) {
                 const int cA = cnA, cB = cnB;
-                cnA = st16[((jb + 2) & 7) * 64 + natoff];
-                cnB = st16[((jb + 3) & 7) * 64 + natoff];
+                cp += 128;
+                cnA = cp[0];
+                cnB = cp[64];
                 const Blk A = prep(cA, jb), B = prep(cB, jb + 1);
                 uint32_t baseB;
                 if (!(A.zrl || B.zrl)) {
@@ -729,11 +735,12 @@ __global__ __launch_bounds__(kWThreads) void stats_wave_kernel(StatsArgs a) {
             }
         }
         JPGE_ACC(2, tq);
-        if ((uint32_t)lane < nb) {  // the DC records
+        if ((uint32_t)lane < nb) {  // the DC records (fields rebuilt from the words kept through the loop)
             srec[bvec] = drec;
-            const uint32_t w = tab_base(2u * tsel) + (uint32_t)dcat;
+            const uint32_t w = ((drec >> 25) ? tab_base(2) : tab_base(0)) + ((drec >> 16) & 0xFFu);
+            const uint32_t rk = (acb & 0x80000000u) | ((acb & 0x7FFFFFFFu) >> 7);  // the text index
             atomicAdd(&cnt[w], 1u);
-            if (rel < L.key[w]) atomicMin(&L.key[w], rel);
+            if (rk < L.key[w]) atomicMin(&L.key[w], rk);
         }
         if (lane == 0) a.tcount[s] = base;
         si = sn;

@@ -127,3 +127,61 @@ def test_batch_share_deals_every_frame_once():
         assert sorted(i for s in shares for i in s) == list(range(256))
         assert max(map(len, shares)) - min(map(len, shares)) <= 1
     assert bench.batch_seed(0) == 1000  # config 4 seeds
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from jpgenc_amd.gather import BatchGather
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, cap = 37, 300  # a batch that does not divide over the ranks; some empty segments
+    g = BatchGather(dist.new_group(backend="gloo"), dist.new_group(backend="gloo"), rank, world, B,
+                    ((B + world - 1) // world) * cap, "cpu")
+
+    def frame_bytes(step, i):  # deterministic stand-in .jpg bytes of frame i at a step
+        gen = torch.Generator().manual_seed(1000 * step + i)
+        n = int(torch.randint(0, cap, (1,), generator=gen)) if i % 7 else 0
+        return torch.randint(0, 256, (n,), dtype=torch.uint8, generator=gen)
+
+    ok = []
+    for step in range(3):  # three posts: both pack buffers, one reused
+        share = g.share(rank)
+        segs, lens = [], []
+        for i in share:
+            b = frame_bytes(step, i)
+            seg = torch.full((cap,), 0xEE, dtype=torch.uint8)  # (slot padding past the bytes)
+            seg[:len(b)] = b
+            segs.append(seg)
+            lens.append(len(b))
+        g.post(segs, lens)
+        if rank == 0:
+            g.wait()
+            ok.append(all(torch.equal(g.frame(i), frame_bytes(step, i)) for i in range(B)))
+    g.wait()
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 3])
+def test_batch_gather_is_byte_equal(world):
+    """Config 4's gather: each rank packs its frames' bytes into one
+    message; rank 0 finds every frame of the batch byte-equal, over three batches
+    (both pack buffers used, one reused)."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    assert res[0] == [True, True, True]
