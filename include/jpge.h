@@ -164,6 +164,15 @@ int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], ui
  * tools): writes n distinct symbols as (symbol, length, code) in DHT order. */
 int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t* codes, int* nsym);
 
+/* The same table build on the GPU (hufftab.hip; the encoder's pipeline runs it on
+ * K2's histograms): nsets sets of the four tables of a frame, host arrays
+ * counts/first [nsets][4][256] in, per table (len << 16) | code [nsets][4][256],
+ * the DHT piece (class/id, bits[16], huffval) [nsets][4][273] and the symbol
+ * count [nsets][4] out.  Replaces generateHuffmanCode (Huffman.hpp:53) on the
+ * device; equal to jpge_huffman_table table by table.  device: the GPU to use. */
+int jpge_huffman_tables_device(int device, const uint32_t* counts, const uint64_t* first, int nsets, uint32_t* tab,
+                               uint8_t* dht, uint32_t* nsym);
+
 /* ---- Decode-side verification utilities (host) ---- */
 
 /* huffmanDecode (Huffman.hpp:62, Huffman.cpp:91-146): the symbol text coded in the

@@ -4,6 +4,7 @@
 #include <pthread.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -17,6 +18,7 @@
 #include "host_io.hpp"
 #include "huffman.hpp"
 #include "ingest.hpp"
+#include "kernels.hpp"
 #include "live.hpp"
 
 struct jpge_ctx {
@@ -250,6 +252,71 @@ int jpge_symbol_stats(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h,
                       uint32_t flags) {
     if (!ctx || !rgb || !qy || !qc || !counts || !first) return JPGE_E_ARG;
     return ctx->enc->symbol_stats(frame(rgb, w, h, stride, maxval), qy, qc, flags, counts, first);
+}
+
+int jpge_huffman_tables_device(int device, const uint32_t* counts, const uint64_t* first, int nsets, uint32_t* tab,
+                               uint8_t* dht, uint32_t* nsym) {
+    if (!counts || !first || nsets <= 0 || !tab || !dht || !nsym) return JPGE_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return JPGE_E_HIP;
+    const size_t n = (size_t)nsets * 1024;
+    std::vector<uint64_t> inv(n);
+    for (size_t i = 0; i < n; ++i) inv[i] = ~first[i];  // (K2's global keys are stored inverted)
+    uint32_t *dc = nullptr, *dtab = nullptr, *dn = nullptr;
+    uint64_t* dk = nullptr;
+    uint8_t* dd = nullptr;
+    int st = JPGE_OK;
+    hipStream_t s = nullptr;
+    if (hipStreamCreate(&s) != hipSuccess || hipMalloc((void**)&dc, n * 4) != hipSuccess ||
+        hipMalloc((void**)&dk, n * 8) != hipSuccess || hipMalloc((void**)&dtab, n * 4) != hipSuccess ||
+        hipMalloc((void**)&dd, (size_t)nsets * 4 * jpge::kDhtPiece) != hipSuccess ||
+        hipMalloc((void**)&dn, (size_t)nsets * 16) != hipSuccess) {
+        st = JPGE_E_HIP;
+    } else {
+        jpge::TabArgs a;
+        a.cnt = dc;
+        a.replicas = 1;
+        a.key = dk;
+        a.tab = dtab;
+        a.dht = dd;
+        a.nsym = dn;
+        a.cnt_stride = 1024;
+        a.key_stride = 1024;
+        a.tab_stride = 1024;
+        a.dht_stride = 4 * jpge::kDhtPiece;
+        a.nsym_stride = 4;
+        uint64_t* ddbg = nullptr;
+        const bool stamps = std::getenv("JPGE_HUFFTAB_STAMPS") != nullptr;  // (diagnostic: phase times to stderr)
+        if (stamps && hipMalloc((void**)&ddbg, (size_t)nsets * 4 * 16 * 8) == hipSuccess) {
+            hipMemsetAsync(ddbg, 0, (size_t)nsets * 4 * 16 * 8, s);
+            a.dbg = ddbg;
+        }
+        if (hipMemcpyAsync(dc, counts, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dk, inv.data(), n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            jpge::launch_huff_tables(a, (uint32_t)nsets, s) != hipSuccess ||
+            hipMemcpyAsync(tab, dtab, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(dht, dd, (size_t)nsets * 4 * jpge::kDhtPiece, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(nsym, dn, (size_t)nsets * 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            st = JPGE_E_HIP;
+        if (ddbg) {
+            std::vector<uint64_t> h((size_t)nsets * 64);
+            hipMemcpy(h.data(), ddbg, h.size() * 8, hipMemcpyDeviceToHost);
+            for (int i = 0; i < nsets * 4; ++i) {
+                std::fprintf(stderr, "hufftab set %d table %d us:", i / 4, i % 4);
+                for (int k = 1; k < 8; ++k)
+                    std::fprintf(stderr, " %.1f", h[i * 16 + k] ? (double)(h[i * 16 + k] - h[i * 16]) / 100.0 : -1.0);
+                std::fprintf(stderr, "\n");
+            }
+            hipFree(ddbg);
+        }
+    }
+    hipFree(dc);
+    hipFree(dk);
+    hipFree(dtab);
+    hipFree(dd);
+    hipFree(dn);
+    if (s) hipStreamDestroy(s);
+    return st;
 }
 
 int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], uint8_t bits[16],
