@@ -76,10 +76,22 @@ inline hipError_t wait_event(hipEvent_t e) {
 //
 // `guess` (napping waits): a running estimate of how long this wait takes at its call
 // site.  The first sleep covers most of it in one wake-up, and naps poll the rest, so
-// a wait of ~100 us costs two or three wake-ups instead of ten.
+// a wait of ~100 us costs two or three wake-ups instead of ten.  The sleep is shortened
+// by twice the waits' spread, so irregular waits (16384^2 frames) are polled, not slept
+// through.
 struct WaitGuess {
     double ema_us = 0;  // smoothed wait duration (0: none yet)
-    double frac = 0;    // first sleep = frac * ema (0: off)
+    double dev_us = 0;  // smoothed |wait - ema_us|
+    double frac = 0;    // first sleep = frac * ema - 2 * dev (0: off)
+    double first_sleep_us() const { return frac * ema_us - 2.0 * dev_us; }
+    void add(double us) {
+        if (ema_us > 0) {
+            dev_us = 0.85 * dev_us + 0.15 * std::fabs(us - ema_us);
+            ema_us = 0.85 * ema_us + 0.15 * us;
+        } else {
+            ema_us = us;
+        }
+    }
     // statistics (JPGE_CPU_PROF): waits, waits already satisfied on entry, naps, total us
     uint64_t waits = 0, ready = 0, naps = 0;
     double total_us = 0;
@@ -100,15 +112,15 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int 
         }
         return kOk;
     }
-    if (nap && guess && guess->frac > 0 && guess->ema_us > 3.0 * nap_us) {
-        std::this_thread::sleep_for(std::chrono::microseconds((long)(guess->frac * guess->ema_us)));
+    if (nap && guess && guess->frac > 0 && guess->first_sleep_us() > 3.0 * nap_us) {
+        std::this_thread::sleep_for(std::chrono::microseconds((long)guess->first_sleep_us()));
         ++guess->naps;
     }
     for (uint32_t spins = 0;; ++spins) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
             if (guess) {
                 const double us = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-                guess->ema_us = guess->ema_us > 0 ? 0.85 * guess->ema_us + 0.15 * us : us;
+                guess->add(us);
                 guess->total_us += us;
             }
             return kOk;
@@ -246,6 +258,7 @@ class Encoder::TablePool {
             auto it = std::find_if(q_.begin(), q_.end(), [](const Job& j) { return j.ready(); });
             if (it != q_.end()) {
                 const double us = std::chrono::duration<double, std::micro>(now - it->submit).count();
+                if (ready_us_ > 0) ready_dev_ = 0.85 * ready_dev_ + 0.15 * std::fabs(us - ready_us_);
                 ready_us_ = ready_us_ > 0 ? 0.85 * ready_us_ + 0.15 * us : us;
                 std::function<void()> run = std::move(it->run);
                 q_.erase(it);
@@ -264,7 +277,7 @@ class Encoder::TablePool {
             if (frac_ > 0 && ready_us_ > 0) {
                 auto first = q_.front().submit;
                 for (const Job& j : q_) first = std::min(first, j.submit);
-                const auto due = first + std::chrono::microseconds((long)(frac_ * ready_us_));
+                const auto due = first + std::chrono::microseconds((long)(frac_ * ready_us_ - 2.0 * ready_dev_));
                 if (due > wake) wake = due;
             }
             lk.unlock();
@@ -281,6 +294,7 @@ class Encoder::TablePool {
     bool polling_ = false;
     double frac_ = 0;      // first sleep, of the usual submit-to-ready delay
     double ready_us_ = 0;  // smoothed submit-to-ready delay of the jobs (upper bound: when first seen ready)
+    double ready_dev_ = 0;  // smoothed |delay - ready_us_|
 };
 
 struct Encoder::Slot {

@@ -57,7 +57,7 @@ void build_code_lengths_std(const std::vector<std::pair<int, int>>& first_order_
             Item a = lv.top(); lv.pop();
             Item b = lv.top(); lv.pop();
             kids.emplace_back(a.node, b.node);
-            nx.push(Item{a.weight + b.weight, n + (int)kids.size() - 1});
+            nx.push(Item{(int)((unsigned)a.weight + (unsigned)b.weight), n + (int)kids.size() - 1});  // (int wrap, as the reference)
         }
     }
     std::vector<int> final_order;
@@ -228,10 +228,13 @@ class HashOrder {
 };
 
 // A heap item: weight in the high word, node id in the low word.  Comparisons look at
-// the weight only (as the reference's comparator), so equal weights never reorder.
+// the weight only (as the reference's comparator), so equal weights never reorder.  The
+// weight is stored with its sign bit flipped, so the high words compare as unsigned
+// numbers in the order of the signed weights (item_hi).
 using HeapItem = uint64_t;
-inline HeapItem item(int w, int node) { return ((uint64_t)(uint32_t)w << 32) | (uint32_t)node; }
-inline int item_w(HeapItem x) { return (int)(x >> 32); }
+inline HeapItem item(int w, int node) { return ((uint64_t)((uint32_t)w ^ 0x80000000u) << 32) | (uint32_t)node; }
+inline int item_w(HeapItem x) { return (int)((uint32_t)(x >> 32) ^ 0x80000000u); }
+inline uint32_t item_hi(HeapItem x) { return (uint32_t)(x >> 32); }
 inline int item_node(HeapItem x) { return (int)(uint32_t)x; }
 // std::push_heap with comp(a, b) = a.w > b.w (libstdc++ __push_heap)
 inline void heap_push(HeapItem* h, int& size, HeapItem v) {
@@ -304,51 +307,139 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         return;
     }
     // package-merge, Huffman.hpp:114-174: 15 levels, each a copy of the leaves' heap
-    // plus the previous level's packages; levels[15] starts empty
+    // plus the previous level's packages; levels[15] starts empty.
+    //
+    // A level is filled completely before it is popped (its packages go to the next
+    // level), and a binary heap pops in weight order, so a level's pop sequence is its
+    // items sorted by weight; the heap decides only the order among EQUAL weights.  The
+    // previous level's packages arrive in non-decreasing weight (sums of consecutive
+    // pops), so the sorted items are a merge of the sorted leaves and those packages.
+    // Consecutive pops pair up into packages, so the order inside a tie matters only
+    // when the tie spans more than one pair (or the unpaired last item; on the final
+    // level, where every pop counts, any tie).  The heap is therefore run only up to
+    // the last such tie of the level; past it the merged order is the pop order (a tie
+    // of two inside one pair only swaps a package's two children, which nothing
+    // downstream distinguishes).  On 4K frames this leaves 0-11% of the reference's
+    // heap pops to simulate.
     constexpr int kLevels = 15, kCap = 2 * kMaxSyms;
     constexpr int kMaxKids = kLevels * kCap, kMaxNodes = kMaxSyms + kMaxKids;
-    // (two level buffers, swapped; padded for heap_pop's look-ahead loads)
-    static thread_local HeapItem base[kMaxSyms], buf0[2 * kCap + kHeapPad], buf1[2 * kCap + kHeapPad];
-    HeapItem *cur = buf0, *nxt = buf1;
+    // (the heap is padded for heap_pop's look-ahead loads; the lists that are merged
+    // carry a sentinel slot at each end: index -1 and index size)
+    static thread_local HeapItem base[kMaxSyms], heap[2 * kCap + kHeapPad], srt_[2 * kCap + 3];
+    static thread_local HeapItem pk_[2][kCap + 2], lsrt_[kMaxSyms + 2];
+    static thread_local uint8_t eq_[2 * kCap + 3];
+    constexpr HeapItem kLo = 0, kHi = ~0ull;  // sentinels: below / above every weight in use
     int nbase = 0;
     for (int i = 0; i < n; ++i) heap_push(base, nbase, item(lcnt[i], i));
+    HeapItem* const lsrt = lsrt_ + 1;  // the leaves by weight
+    HeapItem* const srt = srt_ + 1;    // a level's pop order
+    for (int i = 0; i < n; ++i) lsrt[i] = item(lcnt[i], i);
+    std::sort(lsrt, lsrt + n, [](HeapItem x, HeapItem y) { return item_hi(x) < item_hi(y); });
+    lsrt[-1] = pk_[0][0] = kLo;
+    lsrt[n] = pk_[0][1] = kHi;  // (levels[0]: no packages)
     static thread_local int kid_a[kMaxKids], kid_b[kMaxKids], mult[kMaxNodes], first[kMaxNodes];
-    int nkids = 0;
-    int ncur = nbase;
-    std::copy(base, base + nbase, cur);
-    for (int lv = 0; lv < kLevels; ++lv) {
-        int nn = 0;
-        if (lv + 1 < kLevels) {
-            std::copy(base, base + nbase, nxt);
-            nn = nbase;
+    int nkids = 0, np = 0;
+    // Weights are the reference's ints.  The merges need every weight strictly between the
+    // sentinels; if a package's sum reaches 2^31 - 1 or wraps (counts near 2^31), the
+    // later levels run the heap whole instead.
+    bool wrapped = false;
+    for (int i = 0; i < n; ++i) wrapped |= lcnt[i] <= INT32_MIN + 1 || lcnt[i] >= INT32_MAX;
+    // The end (inclusive) of the last tie in srt[0, m) whose order the heap decides, -1 if
+    // none.  eq[k]: item k weighs the same as item k-1.  A tie between k-1 and k is
+    // harmless only when they are one pair (k odd, below pe = the paired items) and the
+    // tie reaches neither k-2 nor k+1; a harmful tie's later items are harmful too, so
+    // the last harmful k is the end of the last harmful tie.  (Branch-free.)
+    uint8_t* const eq = eq_ + 1;
+    auto last_tie = [srt, eq](int m, int pe) {
+        srt[m] = kHi;
+        for (int k = 0; k <= m; ++k) eq[k] = item_hi(srt[k]) == item_hi(srt[k - 1]);
+        eq[0] = 0;
+        eq[m] = 0;
+        int e = -1;
+        for (int k = 1; k < m; ++k) {
+            const bool h = eq[k] & (!(k & 1) | eq[k - 1] | eq[k + 1] | (k >= pe));
+            e = h ? k : e;
         }
-        while (ncur > 1) {
-            const HeapItem a = heap_pop(cur, ncur), b = heap_pop(cur, ncur);
+        return e;
+    };
+    for (int lv = 0; lv < kLevels; ++lv) {
+        const HeapItem* in = pk_[lv & 1] + 1;
+        HeapItem* out = pk_[(lv + 1) & 1] + 1;
+        const int m = n + np, npairs = m / 2;
+        int e;
+        if (!wrapped) {
+            // levels[lv] = the leaves + levels[lv-1]'s packages, by weight, leaves first on
+            // ties: a branch-free merge run from both ends at once (two independent chains)
+            const int half = (m + 1) / 2;
+            int i = 0, j = 0;
+            for (int k = 0; k < half; ++k) {
+                const HeapItem a = lsrt[i], b = in[j];
+                const bool take = item_hi(b) < item_hi(a);
+                srt[k] = take ? b : a;
+                j += take;
+                i += !take;
+            }
+            i = n - 1;
+            j = np - 1;
+            for (int k = m - 1; k >= half; --k) {
+                const HeapItem a = lsrt[i], b = in[j];
+                const bool take = item_hi(b) >= item_hi(a);
+                srt[k] = take ? b : a;
+                j -= take;
+                i -= !take;
+            }
+            srt[-1] = kLo;
+            e = last_tie(m, m - (m & 1));
+        } else {
+            e = 2 * npairs - 1;
+        }
+        if (e >= 0) {  // the reference's heap up to that tie: the leaves' heap, then the pushes
+            int hn = nbase;
+            std::copy(base, base + nbase, heap);
+            for (int k = 0; k < np; ++k) heap_push(heap, hn, in[k]);
+            for (int k = 0; k <= e; ++k) srt[k] = heap_pop(heap, hn);
+        }
+        for (int k = 0; k < npairs; ++k) {
+            const HeapItem a = srt[2 * k], b = srt[2 * k + 1];
             kid_a[nkids] = item_node(a);
             kid_b[nkids] = item_node(b);
-            heap_push(nxt, nn, item(item_w(a) + item_w(b), n + nkids));
+            const int64_t sum = (int64_t)item_w(a) + item_w(b);
+            wrapped |= sum >= INT32_MAX || sum <= INT32_MIN + 1;
+            out[k] = item((int32_t)(uint32_t)sum, n + nkids);
             ++nkids;
         }
-        std::swap(cur, nxt);
-        ncur = nn;
+        out[-1] = kLo;
+        out[npairs] = kHi;
+        np = npairs;
     }
-    // cur: levels[15]; pop order = the final packages.  Push the multiplicities and the
-    // first final package down the DAG (a package's id exceeds its children's).
+    // levels[15]: levels[14]'s packages alone, pushed in non-decreasing weight, so its
+    // heap array is the push order; its pop order = the final packages.  (Every pop
+    // counts here, so every tie is the heap's.)
+    const HeapItem* fin = pk_[kLevels & 1] + 1;
+    std::copy(fin, fin + np, srt);
+    srt[-1] = kLo;
+    const int e = wrapped ? np - 1 : last_tie(np, 0);
+    if (e >= 0) {
+        int hn = 0;
+        for (int k = 0; k < np; ++k) heap_push(heap, hn, fin[k]);
+        for (int k = 0; k <= e; ++k) srt[k] = heap_pop(heap, hn);
+    }
+    // Push the multiplicities and the first final package down the DAG (a package's id
+    // exceeds its children's).
     const int total = n + nkids;
     std::fill(mult, mult + total, 0);
     std::fill(first, first + total, INT32_MAX);
-    for (int k = 0; ncur > 0; ++k) {
-        const int f = item_node(heap_pop(cur, ncur));
+    for (int k = 0; k < np; ++k) {
+        const int f = item_node(srt[k]);
         mult[f] += 1;
         if (k < first[f]) first[f] = k;
     }
-    for (int id = total - 1; id >= n; --id) {
-        if (!mult[id]) continue;
+    for (int id = total - 1; id >= n; --id) {  // (unused packages add 0: no branch)
         const int ka = kid_a[id - n], kb = kid_b[id - n];
         mult[ka] += mult[id];
         mult[kb] += mult[id];
-        if (first[id] < first[ka]) first[ka] = first[id];
-        if (first[id] < first[kb]) first[kb] = first[id];
+        first[ka] = std::min(first[ka], first[id]);
+        first[kb] = std::min(first[kb], first[id]);
     }
     // code_lengths (an unordered_map) receives symbols by (first package, symbol)
     int ins[kMaxSyms];
