@@ -459,6 +459,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
+    e->set_ = env_int("JPGE_SET", 0, 0, kMaxSet);
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
     e->inline_tables_ = env_int("JPGE_INLINE_TABLES", 2, 0, 2);
     e->nap_us_ = env_int("JPGE_NAP_US", e->nap_us_, 1, 1000);
@@ -509,26 +510,31 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
         }
         JPGE_HIP(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
         ln->guess_hist.frac = ln->guess_result.frac = e->first_sleep_;
-        for (int i = 0; i < nslots; ++i) {
-            std::unique_ptr<Slot> s(new Slot());
-            s->stream = ln->stream;
-            s->guess_hist = &ln->guess_hist;
-            s->guess_result = &ln->guess_result;
-            for (int k = 0; k < 8; ++k)
-                JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], hipEventDefault));
-            JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
-            JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
-            JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
-            JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_tab_host, s->h_tab, 0));
-            JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
-            JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
-            JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
-            ln->slots.push_back(std::move(s));
-        }
+        if (const int st = e->add_slots(*ln, nslots)) return st;
         if (l > 0) ln->start();
         e->lanes_.push_back(std::move(ln));
     }
     out = std::move(e);
+    return kOk;
+}
+
+int Encoder::add_slots(Lane& ln, int count) {
+    while ((int)ln.slots.size() < count) {
+        std::unique_ptr<Slot> s(new Slot());
+        s->stream = ln.stream;
+        s->guess_hist = &ln.guess_hist;
+        s->guess_result = &ln.guess_result;
+        for (int k = 0; k < 8; ++k)
+            JPGE_HIP(hipEventCreateWithFlags(&s->ev[k], hipEventDefault));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_hist, sizeof(HostHist), hipHostMallocMapped));
+        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
+        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_tab_host, s->h_tab, 0));
+        JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
+        JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
+        JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
+        ln.slots.push_back(std::move(s));
+    }
     return kOk;
 }
 
@@ -725,8 +731,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
 }
 
 // Phase 1: upload (if host input), statistics kernels, histogram read-back.
-int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
-                    Slot* imp, bool export_hist) {
+int Encoder::prep1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
+                   Slot* imp, FdctArgs& a, StatsArgs& st) {
     if (!f.rgb || f.width == 0 || f.height == 0 || f.width > 65535 || f.height > 65535) return kErrArg;
     if (f.maxval < 1 || f.maxval > 255) return kErrRange;
     const Geometry g = geometry(f.width, f.height, mode_);
@@ -738,8 +744,8 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     const size_t out_cap = (flags & kFlagDeviceOutput) ? 0 : max_jpeg_bytes(f.width, f.height);
     for (int i = 0; i < 64; ++i)
         if (!qy[i] || !qc[i]) return kErrArg;
-    const int st = ensure(s, g, in_bytes, out_cap);
-    if (st) return st;
+    const int st0 = ensure(s, g, in_bytes, out_cap);
+    if (st0) return st0;
     std::memcpy(s.qy, qy, 64);
     std::memcpy(s.qc, qc, 64);
     s.g = g;
@@ -767,11 +773,19 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.key_y0 = s.key_c0 = s.key_ncb = 0;
     s.img_w = f.width;
     s.img_h = f.height;
-    const FdctArgs a = fdct_args(s, f.maxval, imp);
-    const StatsArgs st2 = stats_args(s);
-    s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
+    a = fdct_args(s, f.maxval, imp);
+    st = stats_args(s);
     s.tables_done.store(0, std::memory_order_relaxed);
     s.export_queued.store(0, std::memory_order_relaxed);
+    return kOk;
+}
+
+int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags,
+                    Slot* imp, bool export_hist) {
+    FdctArgs a;
+    StatsArgs st2;
+    if (const int st = prep1(s, f, qy, qc, flags, imp, a, st2)) return st;
+    s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
     // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
     const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
     JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
@@ -783,6 +797,20 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
                                     s.stream));
         s.export_queued.store(1, std::memory_order_release);
+    }
+    return kOk;
+}
+
+// A frame set's phase 1: the members' arguments come from prep1 (members it refused
+// are not in the set).  Their histograms leave through a later code kernel or
+// launch_hist_export.
+int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a, const StatsArgs* st) {
+    for (int m = 0; m < n; ++m) s[m]->timed = false;  // (no per-frame kernel events in a set)
+    JPGE_HIP(launch_fdct_set(a, n, s[0]->stream));
+    JPGE_HIP(launch_stats_set(st, n, s[0]->stream));
+    for (int m = 0; m < n; ++m) {
+        s[m]->seq = ++seq_counter_;
+        s[m]->hist = st[m].hist;
     }
     return kOk;
 }
@@ -945,19 +973,23 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
     if (inline_tables_ != 1 && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_, first_sleep_));
-    // Frames are dealt dynamically: a lane takes the batch's next frame when its
-    // pipeline has room, so lanes finish together.  Lane 0 runs on the calling thread.
-    const int nl = std::min<int>((int)lanes_.size(), n);
+    // Frames are dealt dynamically: a lane takes the batch's next frame (or frame set)
+    // when its pipeline has room, so lanes finish together.  Lane 0 runs on the calling
+    // thread.
+    const int set = batch_set_size(fr, n);
+    const int nl = std::min<int>((int)lanes_.size(), (n + set - 1) / set);
+    for (int l = 0; l < nl; ++l)
+        if (const int st = add_slots(*lanes_[l], (lookahead_ + drain_lag_ + 1) * set)) return st;
     std::atomic<int> next{0};
     for (int l = 1; l < nl; ++l)
-        lanes_[l]->post([this, l, fr, n, &next, qy, qc, flags] {
+        lanes_[l]->post([this, l, fr, n, &next, set, qy, qc, flags] {
             hipSetDevice(device_);
-            return run_lane(*lanes_[l], fr, n, &next, qy, qc, flags);
+            return run_lane(*lanes_[l], fr, n, &next, set, qy, qc, flags);
         });
     // (napping on the calling thread: ~1 us timer slack for the call, restored after)
     const long slack = nap_ ? prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0) : -1;
     if (slack > 0) prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
-    int st = run_lane(*lanes_[0], fr, n, &next, qy, qc, flags);
+    int st = run_lane(*lanes_[0], fr, n, &next, set, qy, qc, flags);
     if (slack > 0) prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
     const auto t_lane0 = std::chrono::steady_clock::now();
     for (int l = 1; l < nl; ++l) {
@@ -982,25 +1014,49 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     return st;
 }
 
-int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* next, const uint8_t qy[64],
+// Frames per launch: sets of frames of one small geometry (kernels.hpp FrameSet), about
+// a 4K frame's pixels per launch.  A set's entropy launch needs every member placed by
+// its own last code workgroup (the pipeline's placement mode, no restart intervals).
+constexpr uint64_t kSetPixels = 3840ull * 2160ull;
+int Encoder::batch_set_size(const FrameDesc* fr, int n) const {
+    if (n < 2 || set_ == 1) return 1;
+    const FrameDesc& f0 = fr[0];
+    if (!f0.width || !f0.height || f0.width > 65535 || f0.height > 65535) return 1;
+    for (int i = 1; i < n; ++i)
+        if (fr[i].width != f0.width || fr[i].height != f0.height || (fr[i].maxval == 255) != (f0.maxval == 255))
+            return 1;
+    const bool placed_in_code = (ext_place_ > 0 || (ext_place_ < 0 && lanes_.size() > 1)) && place_in_code_;
+    if (!placed_in_code || restart_mcus_ || layout(geometry(f0.width, f0.height, mode_)).grid() > kPlaceInCodeMaxWgs)
+        return 1;
+    if (set_) return set_;
+    const uint64_t k = kSetPixels / ((uint64_t)f0.width * f0.height);
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(kMaxSet, k));
+}
+
+int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* next, int set, const uint8_t qy[64],
                       const uint8_t qc[64], uint32_t flags) {
-    const int S = (int)ln.slots.size();
+    const int S = (int)ln.slots.size() / set;  // slot sets (add_slots: >= lookahead + drain lag + 1)
+    // Pipeline step t handles frame set t of this lane: frames mine[t*set ..], each in
+    // slot (t mod S) * set + member.  Only the lane's last set may be short.
     std::vector<int> mine;  // batch indices of the frames this lane took, in its order
     mine.reserve(total);
-    auto frame = [&](int t) -> FrameDesc& { return frames[mine[t]]; };
+    auto members = [&](int t) { return std::min(set, (int)mine.size() - t * set); };
+    auto frame = [&](int t, int m) -> FrameDesc& { return frames[mine[t * set + m]]; };
+    auto slot = [&](int t, int m) -> Slot& { return *ln.slots[(t % S) * set + m]; };
     int first_err = kOk;
-    auto note = [&](int t, int st) {
-        if (st && !frame(t).status) frame(t).status = st;
+    auto note = [&](int t, int m, int st) {
+        if (st && !frame(t, m).status) frame(t, m).status = st;
         if (st && !first_err) first_err = st;
     };
-    // Software pipeline on the lane's stream (frame numbers are lane-local).  Iteration i queues
-    //   K1(i) [carrying frame j = i-L's tables + headers to the device], K2(i),
-    //   then frame j's entropy kernels [the code kernel carrying frame i's
-    //   histograms to the host for a table worker],
-    // so the host builds a frame's tables while the GPU works through the L frames
-    // queued ahead of its entropy launch; frame i-L-D is drained D iterations after
-    // that launch (about D frames of queued GPU work while the host waits).  The
-    // pipeline's edges fall back to a standalone export kernel and a table copy.
+    // Software pipeline on the lane's stream (steps are lane-local).  Step i queues
+    //   K1(i) [carrying set j = i-L's tables + headers to the device], K2(i),
+    //   then set j's entropy kernels [the code kernel carrying set i's histograms to
+    //   the host for a table worker],
+    // so the host builds a set's tables while the GPU works through the L sets queued
+    // ahead of its entropy launch; set i-L-D is drained D steps after that launch (about
+    // D sets of queued GPU work while the host waits).  Member m of one set pairs with
+    // member m of the other for the carried duties.  The pipeline's edges fall back to a
+    // standalone export kernel and a table copy.
     const int L = lookahead_, D = drain_lag_;
     auto submit_tables = [&](Slot& s) {
         // Large frames: built by this lane's thread when the frame's entropy launch needs
@@ -1033,7 +1089,7 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
                            {}});
         }
     };
-    // diagnostic host trace: (iteration, point, us since the call, and at point 1 the
+    // diagnostic host trace: (step, point, us since the call, and at point 1 the
     // awaited table job's submit / start / done times)
     std::vector<std::array<double, 6>> trace;
     const auto t_call = std::chrono::steady_clock::now();
@@ -1060,13 +1116,13 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
                              job ? us(job->t_submit) : 0.0, job ? us(job->t_start) : 0.0,
                              job ? us(job->t_done) : 0.0});
     };
-    int n = 0;         // frames taken so far
+    int n = 0;         // sets taken so far
     bool open = true;  // the batch may still have frames
     for (int i = 0;; ++i) {
-        if (open && i == n) {  // room for a new frame: take the batch's next one
-            const int g = next->fetch_add(1, std::memory_order_relaxed);
+        if (open && i == n) {  // room for a new set: take the batch's next frames
+            const int g = next->fetch_add(set, std::memory_order_relaxed);
             if (g < total) {
-                mine.push_back(g);
+                for (int m = 0; m < set && g + m < total; ++m) mine.push_back(g + m);
                 ++n;
             } else {
                 open = false;
@@ -1075,56 +1131,137 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         if (!open && i >= n + L + D) break;
         const int j = i - L, k = i - L - D;
         mark(i, 0);
-        Slot* sj = nullptr;  // frame j, tables built, ready for its entropy kernels
-        if (j >= 0 && j < n && !frame(j).status) {
-            Slot& s = *ln.slots[j % S];
-            if (s.inline_tables && !s.tables_done.load(std::memory_order_acquire)) {
-                // (no pool: a single-frame encode builds its four tables in parallel)
-                s.tables_status = build_tables(s, /*parallel=*/!pool_);
-                s.tables_done.store(1, std::memory_order_release);
+        Slot* sj[kMaxSet] = {};  // set j's members, tables built, ready for their entropy kernels
+        if (j >= 0 && j < n) {
+            for (int m = 0; m < members(j); ++m) {
+                if (frame(j, m).status) continue;
+                Slot& s = slot(j, m);
+                if (s.inline_tables && !s.tables_done.load(std::memory_order_acquire)) {
+                    // (no pool: a single-frame encode builds its four tables in parallel)
+                    s.tables_status = build_tables(s, /*parallel=*/!pool_);
+                    s.tables_done.store(1, std::memory_order_release);
+                }
+                while (!s.tables_done.load(std::memory_order_acquire)) {
+                    if (nap_) std::this_thread::sleep_for(std::chrono::microseconds(nap_us_));
+                    else std::this_thread::yield();
+                }
+                if (s.tables_status) note(j, m, s.tables_status);
+                else sj[m] = &s;
             }
-            while (!s.tables_done.load(std::memory_order_acquire)) {
-                if (nap_) std::this_thread::sleep_for(std::chrono::microseconds(nap_us_));
-                else std::this_thread::yield();
-            }
-            if (s.tables_status) note(j, s.tables_status);
-            else sj = &s;
-            mark(i, 1, &s);
+            mark(i, 1, sj[0]);
         } else {
             mark(i, 1);
         }
-        Slot* si = nullptr;  // frame i, whose histograms still need exporting
-        bool imported = false;
+        Slot* si[kMaxSet] = {};  // set i's members whose histograms set j's code kernels export
+        bool imported[kMaxSet] = {};
         if (i < n) {
-            Slot& s = *ln.slots[i % S];
-            note(i, phase1(s, frame(i), qy, qc, flags, sj, /*export_hist=*/sj == nullptr));
-            if (!frame(i).status) {
-                imported = sj != nullptr;
-                si = sj ? &s : nullptr;
-                submit_tables(s);
+            const int mi = members(i);
+            if (set == 1) {
+                Slot& s = slot(i, 0);
+                note(i, 0, phase1(s, frame(i, 0), qy, qc, flags, sj[0], /*export_hist=*/sj[0] == nullptr));
+                if (!frame(i, 0).status) {
+                    imported[0] = sj[0] != nullptr;
+                    si[0] = sj[0] ? &s : nullptr;
+                    submit_tables(s);
+                }
+            } else {
+                Slot* ss[kMaxSet];
+                FdctArgs fa[kMaxSet];
+                StatsArgs sa[kMaxSet];
+                int ms[kMaxSet], ok = 0;
+                for (int m = 0; m < mi; ++m) {
+                    Slot& s = slot(i, m);
+                    const int st = prep1(s, frame(i, m), qy, qc, flags, sj[m], fa[ok], sa[ok]);
+                    note(i, m, st);
+                    if (st) continue;
+                    ss[ok] = &s;
+                    ms[ok++] = m;
+                }
+                if (ok) {
+                    const int st = phase1_set(ss, ok, fa, sa);
+                    for (int q = 0; q < ok; ++q) {
+                        const int m = ms[q];
+                        note(i, m, st);
+                        if (st) continue;
+                        Slot& s = slot(i, m);
+                        imported[m] = sj[m] != nullptr;
+                        if (sj[m]) {
+                            si[m] = &s;
+                        } else {  // (no code kernel of set j to carry the export)
+                            const hipError_t e = launch_hist_export(s.hist, s.d_hist_host->cnt, s.d_hist_host->key,
+                                                                    &s.d_hist_host->seq, s.seq, s.stream);
+                            note(i, m, e == hipSuccess ? kOk : kErrHip);
+                            if (e == hipSuccess) s.export_queued.store(1, std::memory_order_release);
+                        }
+                        if (!frame(i, m).status) submit_tables(s);
+                    }
+                }
             }
         }
         mark(i, 2);
-        if (sj) {
-            int st = imported ? kOk : import_tables_copy(*sj);
-            if (!st) st = launch_entropy_phase(*sj, si);
-            note(j, st);
-            if (!st && si) {  // exported by frame j's code kernel
-                si->export_queued.store(1, std::memory_order_release);
-                si = nullptr;
+        if (j >= 0 && j < n) {
+            // set j's entropy kernels: one launch per kernel for the set, or frame by frame
+            // (a single frame; a member its code kernel does not place)
+            EntropyArgs ea[kMaxSet];
+            int ms[kMaxSet], ne = 0;
+            bool as_set = set > 1;
+            for (int m = 0; m < members(j); ++m) {
+                if (!sj[m]) continue;
+                const int st = imported[m] ? kOk : import_tables_copy(*sj[m]);
+                note(j, m, st);
+                if (st) {
+                    sj[m] = nullptr;
+                    continue;
+                }
+                ea[ne] = entropy_args(*sj[m]);
+                if (Slot* ex = si[m] && !frame(i, m).status ? si[m] : nullptr) {  // (carried export)
+                    ea[ne].exp_hist = ex->hist;
+                    ea[ne].exp_cnt = ex->d_hist_host->cnt;
+                    ea[ne].exp_key = ex->d_hist_host->key;
+                    ea[ne].exp_seq = &ex->d_hist_host->seq;
+                    ea[ne].exp_seqv = ex->seq;
+                }
+                as_set = as_set && ea[ne].done;
+                ms[ne++] = m;
+            }
+            if (ne) {
+                if (as_set) {
+                    for (int q = 0; q < ne; ++q) sj[ms[q]]->h_result[2] = 0;
+                    const hipError_t e = launch_entropy_set(ea, ne, sj[ms[0]]->stream);
+                    for (int q = 0; q < ne; ++q) note(j, ms[q], e == hipSuccess ? kOk : kErrHip);
+                    if (e != hipSuccess) ne = 0;
+                } else {
+                    for (int q = 0; q < ne; ++q) {
+                        const int m = ms[q];
+                        const int st = launch_entropy_phase(*sj[m], si[m] && !frame(i, m).status ? si[m] : nullptr);
+                        note(j, m, st);
+                        if (st) sj[m] = nullptr;
+                    }
+                }
+                for (int q = 0; q < ne; ++q) {  // exported by member m of set j's code kernel
+                    const int m = ms[q];
+                    if (sj[m] && si[m] && !frame(i, m).status) {
+                        si[m]->export_queued.store(1, std::memory_order_release);
+                        si[m] = nullptr;
+                    }
+                }
             }
         }
         mark(i, 3);
-        if (si) {  // (frame j failed: export frame i's histograms on their own)
-            const hipError_t e = launch_hist_export(si->hist, si->d_hist_host->cnt, si->d_hist_host->key,
-                                                    &si->d_hist_host->seq, si->seq, si->stream);
-            note(i, e == hipSuccess ? kOk : kErrHip);
-            if (e == hipSuccess) si->export_queued.store(1, std::memory_order_release);
+        for (int m = 0; m < kMaxSet; ++m) {  // (no carrier: export set i's histograms on their own)
+            Slot* s = si[m];
+            if (!s) continue;
+            const hipError_t e = launch_hist_export(s->hist, s->d_hist_host->cnt, s->d_hist_host->key,
+                                                    &s->d_hist_host->seq, s->seq, s->stream);
+            note(i, m, e == hipSuccess ? kOk : kErrHip);
+            if (e == hipSuccess) s->export_queued.store(1, std::memory_order_release);
         }
         if (k >= 0 && k < n) {
-            Slot& s = *ln.slots[k % S];
-            if (!frame(k).status) note(k, finish(s, frame(k), flags));
-            else hipStreamSynchronize(s.stream);
+            for (int m = 0; m < members(k); ++m) {
+                Slot& s = slot(k, m);
+                if (!frame(k, m).status) note(k, m, finish(s, frame(k, m), flags));
+                else hipStreamSynchronize(s.stream);
+            }
         }
         mark(i, 4);
     }
@@ -1137,10 +1274,10 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         if (end_sync_ == 1) JPGE_HIP(hipEventSynchronize(ln.done));
         else JPGE_HIP(wait_event(ln.done));
     }
-    mark(n + L + D, 5);  // (n: this lane's frame count)
+    mark(n + L + D, 5);  // (n: this lane's set count)
     if (cpu_prof_) {
-        for (int k = 0; k < 6; ++k) cpu_ns_[k].fetch_add(cpu_acc[k], std::memory_order_relaxed);
-        cpu_frames_.fetch_add(n, std::memory_order_relaxed);
+        for (int q = 0; q < 6; ++q) cpu_ns_[q].fetch_add(cpu_acc[q], std::memory_order_relaxed);
+        cpu_frames_.fetch_add((int64_t)mine.size(), std::memory_order_relaxed);
     }
     if (host_trace_file_) {
         std::lock_guard<std::mutex> g(trace_mu_);

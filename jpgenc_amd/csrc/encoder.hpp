@@ -130,6 +130,17 @@ class Encoder {
     // (carries `imp`'s tables to the device; exports its own histograms if asked)
     int phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags, Slot* imp,
                bool export_hist);
+    // phase 1's host half: validate, size the slot, record the frame's state, the kernels' arguments
+    int prep1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], uint32_t flags, Slot* imp,
+              FdctArgs& a, StatsArgs& st);
+    // phase 1 of a frame set (kernels.hpp FrameSet: one transform and one statistics
+    // launch for n frames of one geometry, prepared by prep1)
+    int phase1_set(Slot* const* s, int n, const FdctArgs* a, const StatsArgs* st);
+    // frames per launch for a batch: kMaxSet when every frame has one small geometry
+    // (JPGE_SET: 1..kMaxSet forces a size), else 1
+    int batch_set_size(const FrameDesc* fr, int n) const;
+    // a lane's slots: at least `count`
+    int add_slots(Lane& ln, int count);
     // phase 2a (host, any thread): Huffman tables + headers from the histograms
     int build_tables(Slot& s, bool parallel);
     int build_tables_from(Slot& s, const uint32_t* cnt, const uint64_t* first, bool parallel);
@@ -141,7 +152,8 @@ class Encoder {
     int launch_entropy_phase(Slot& s, Slot* exp);
     int finish(Slot& s, FrameDesc& f, uint32_t flags);
     // one lane's software pipeline over the frames it takes from fr[0..total) through `next`
-    int run_lane(Lane& ln, FrameDesc* fr, int total, std::atomic<int>* next, const uint8_t qy[64],
+    // (frames go in sets of `set` when set > 1: a pipeline step is a set, one launch per kernel)
+    int run_lane(Lane& ln, FrameDesc* fr, int total, std::atomic<int>* next, int set, const uint8_t qy[64],
                  const uint8_t qc[64], uint32_t flags);
 
     int device_ = 0;
@@ -169,6 +181,7 @@ class Encoder {
     uint32_t fdct_wgs_ = 0;     // JPGE_FDCT_WGS: pipeline transform grid (0: fdct_grid's cap)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
+    int set_ = 0;               // JPGE_SET: frames per launch (0: batch_set_size decides)
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables (JPGE_INLINE_TABLES=0)
     int inline_tables_ = 2;     // JPGE_INLINE_TABLES: 1 each lane's thread builds its frames' tables, 0 the
                                 // pool, 2 (default) by frame size (encoder.cpp kInlineTablesMinPixels)

@@ -104,10 +104,12 @@ __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, ui
 __device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int tid);
 
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_WPE))) void entropy_code_kernel(
-    EntropyArgs a) {
+    FrameSet<EntropyArgs> fs) {
     __shared__ K3Lds L;
+    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const EntropyArgs& a = fs.a[set_f];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t wg = blockIdx.x;
+    const uint32_t wg = blockIdx.x - fs.wg0[set_f], G = fs.wg0[set_f + 1] - fs.wg0[set_f];
     JPGE_STAMP(0);
     if (a.exp_cnt && wg == 0)  // carried: a later frame's histograms to the host
         export_hist<kK3Threads>(a.exp_hist, a.exp_cnt, a.exp_key, a.exp_seq, a.exp_seqv, tid);
@@ -366,11 +368,11 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         // kernel and the pack kernel): every workgroup counts itself after its record is
         // visible device-wide; the one that completes the count reads all records.
         __syncthreads();
-        if (tid == 0) L.carry = atomicAdd(a.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+        if (tid == 0) L.carry = atomicAdd(a.done, 1u) == G - 1 ? 1u : 0u;
         __syncthreads();
         if (L.carry) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the other workgroups' records)
-            place_all(a, gridDim.x, &L.wsum[0][0], tid);
+            place_all(a, G, &L.wsum[0][0], tid);
         }
     }
     JPGE_STAMP(2);
@@ -622,10 +624,12 @@ struct PackLds {
     uint32_t Lb, ftotal, split, fill, seg;
 };
 
-__global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(EntropyArgs a) {
+__global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<EntropyArgs> fs) {
     __shared__ PackLds S;
+    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const EntropyArgs& a = fs.a[set_f];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t wg = blockIdx.x, G = gridDim.x;
+    const uint32_t wg = blockIdx.x - fs.wg0[set_f], G = fs.wg0[set_f + 1] - fs.wg0[set_f];
     const bool last = wg == G - 1;
     const bool eoi = last && (a.flags & kStripeLast);
     // the workgroup 1-fills its final byte: the image's end, or (restart) its segment's
@@ -818,7 +822,7 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
 
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tcode, const KTimer* tpack) {
     const uint32_t G = a.seg.grid();
-    hipError_t e = launch_timed(tcode, entropy_code_kernel, dim3(G), dim3(kK3Threads), s, a);
+    hipError_t e = launch_timed(tcode, entropy_code_kernel, dim3(G), dim3(kK3Threads), s, frame_set(&a, 1, G));
     if (e != hipSuccess) return e;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
@@ -830,13 +834,32 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tco
         b.flags |= kExtPlace;
         if ((e = launch_place(b, G, s)) != hipSuccess) return e;
     }
-    return launch_timed(tpack, entropy_pack_kernel, dim3(G), dim3(kK3Threads), s, b);
+    return launch_timed(tpack, entropy_pack_kernel, dim3(G), dim3(kK3Threads), s, frame_set(&b, 1, G));
+}
+
+hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s) {
+    if (n < 1 || n > kMaxSet) return hipErrorInvalidValue;
+    const uint32_t G = a[0].seg.grid();
+    FrameSet<EntropyArgs> fs = frame_set(a, n, G);
+    for (int f = 0; f < n; ++f) {  // one partition, each member placed by its code kernel's last workgroup
+        const EntropyArgs& m = a[f];
+        if (m.seg.grid() != G || !m.done || !m.place || m.rst.mcus || G > kPlaceInCodeMaxWgs) return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(entropy_code_kernel, dim3(G * n), dim3(kK3Threads), 0, s, fs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    for (int f = 0; f < n; ++f) {
+        fs.a[f].flags |= kExtPlace;
+        fs.a[f].dbg = a[f].dbg ? a[f].dbg + 65536 * kStampSlots : nullptr;
+    }
+    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G * n), dim3(kK3Threads), 0, s, fs);
+    return hipGetLastError();
 }
 
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
     const uint32_t G = a.seg.grid();
     if (!a.summary) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, a);
+    hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, frame_set(&a, 1, G));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // (restart intervals: the stripe's placement is its own, computed now; its summary
@@ -854,7 +877,7 @@ hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s) {
         const hipError_t e = launch_place(b, G, s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, b);
+    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, frame_set(&b, 1, G));
     return hipGetLastError();
 }
 

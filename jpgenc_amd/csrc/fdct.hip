@@ -18,6 +18,8 @@
 // no contraction (-ffp-contract=off plus the pragma in device_common.hpp); the
 // colour conversion of 8-bit input uses FMA chains only where every partial result
 // is exact (all terms are multiples of 2^-27 far inside 53 bits).
+#include <cstring>
+
 #include "arai.hpp"
 #include "device_common.hpp"
 
@@ -173,7 +175,10 @@ __device__ __forceinline__ void swap_halves(double& a, double& b) {
 }
 
 template <bool kExact, int kWaves, int kFilt>
-__global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
+__global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs> fs) {
+    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const FdctArgs& a = fs.a[set_f];
+    const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
     constexpr int kK1Threads = kWaves * 64;
     __shared__ K1Lds<kWaves> lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;  // wv: 0..15
@@ -202,8 +207,8 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     // counter until the run is exhausted.  The SIMD issues the oldest ready wave
     // first, so waves progress unequally: grabbing lets the faster ones take more
     // tiles, and all waves of a CU finish within about a tile of each other.
-    const uint32_t tb_p = (uint32_t)((uint64_t)ntiles * blockIdx.x / gridDim.x);
-    const uint32_t n_p = (uint32_t)((uint64_t)ntiles * (blockIdx.x + 1) / gridDim.x) - tb_p;
+    const uint32_t tb_p = (uint32_t)((uint64_t)ntiles * bid / nbk);
+    const uint32_t n_p = (uint32_t)((uint64_t)ntiles * (bid + 1) / nbk) - tb_p;
     auto grab = [&]() -> uint32_t {
         uint32_t v = 0;
         if (lane == 0) v = atomicAdd(&lds.next, 1u);
@@ -237,8 +242,8 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FdctArgs a) {
     uint4 c0, c1, c2;
     bool cfast = fast_load(k, c0, c1, c2);  // issued before the prologue's own memory traffic
 
-    for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
-    if (blockIdx.x == 0)  // carried: another frame's tables + headers, host -> device
+    for (uint32_t i = bid * kK1Threads + tid; i < a.zero_words; i += nbk * kK1Threads) a.zero[i] = 0;
+    if (bid == 0)  // carried: another frame's tables + headers, host -> device
         for (uint32_t i = tid; i < a.imp_n16; i += kK1Threads) a.imp_dst[i] = a.imp_src[i];
     if (tid == 0) lds.next = kWaves;
     if (tid < 128) {
@@ -468,7 +473,10 @@ constexpr int kRgbPitch444 = 130;  // u32 per staged row of 128 px (+2: even, fo
 static_assert(8 * kRgbPitch444 <= 16 * kRgbPitch, "the 4:4:4 tile fits the 4:2:0 staging area");
 
 template <bool kExact, int kWaves, int kYh>
-__global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
+__global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArgs> fs) {
+    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const FdctArgs& a = fs.a[set_f];
+    const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
     constexpr int kK1Threads = kWaves * 64;
     constexpr uint32_t kMcus = 16 / kYh;            // MCUs per tile
     constexpr int kBpm = kYh + 2;                   // blocks per MCU
@@ -492,8 +500,8 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
         __builtin_amdgcn_make_buffer_rsrc(a.coef, 0, (int)(uint32_t)((uint64_t)a.g.nblocks() * 128), 0x00020000);
 
     // dynamic tiles over the workgroup's contiguous run, as in fdct_kernel
-    const uint32_t tb_p = (uint32_t)((uint64_t)ntiles * blockIdx.x / gridDim.x);
-    const uint32_t n_p = (uint32_t)((uint64_t)ntiles * (blockIdx.x + 1) / gridDim.x) - tb_p;
+    const uint32_t tb_p = (uint32_t)((uint64_t)ntiles * bid / nbk);
+    const uint32_t n_p = (uint32_t)((uint64_t)ntiles * (bid + 1) / nbk) - tb_p;
     auto grab = [&]() -> uint32_t {
         uint32_t v = 0;
         if (lane == 0) v = atomicAdd(&lds.next, 1u);
@@ -519,8 +527,8 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FdctArgs a) {
     uint4 c0, c1, c2;
     bool cfast = fast_load(k, c0, c1, c2);
 
-    for (uint32_t i = blockIdx.x * kK1Threads + tid; i < a.zero_words; i += gridDim.x * kK1Threads) a.zero[i] = 0;
-    if (blockIdx.x == 0)
+    for (uint32_t i = bid * kK1Threads + tid; i < a.zero_words; i += nbk * kK1Threads) a.zero[i] = 0;
+    if (bid == 0)
         for (uint32_t i = tid; i < a.imp_n16; i += kK1Threads) a.imp_dst[i] = a.imp_src[i];
     if (tid == 0) lds.next = kWaves;
     if (tid < 128) {
@@ -661,26 +669,28 @@ uint32_t k1_tiles(const Geometry& g) {
 bool k1_whole_cu(const Geometry& g, bool solo) { return solo && k1_tiles(g) >= kK1WholeCuTiles; }
 
 template <int kYh>
-hipError_t launch_row8(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
+hipError_t launch_row8(const FrameSet<FdctArgs>& fs, uint32_t grid, hipStream_t s, const KTimer* t) {
+    const FdctArgs& a = fs.a[0];
     const bool ex = a.maxval == 255;
     if (k1_whole_cu(a.g, a.solo)) {
-        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
-        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
+        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
     } else {
-        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
-        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
+        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
     }
 }
 
 template <int kFilt>
-hipError_t launch_420(const FdctArgs& a, uint32_t grid, hipStream_t s, const KTimer* t) {
+hipError_t launch_420(const FrameSet<FdctArgs>& fs, uint32_t grid, hipStream_t s, const KTimer* t) {
+    const FdctArgs& a = fs.a[0];
     const bool ex = a.maxval == 255;
     if (k1_whole_cu(a.g, a.solo)) {
-        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
-        else return launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, a);
+        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
+        else return launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
     } else {
-        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
-        else return launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, a);
+        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
+        else return launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
     }
 }
 
@@ -697,28 +707,45 @@ uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs) {
     return wgs < cap ? wgs : cap;
 }
 
-hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
-    // 32-bit buffer offsets: the frame's pixels and coefficients must stay below kOob
-    // (a 16384^2 frame needs 805 MB of each)
-    if ((uint64_t)a.stride * a.g.height >= kOob || (uint64_t)a.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
-    const uint32_t grid = fdct_grid(a.g, a.solo, a.wgs);
+// A set of frames of one geometry, colour path and workgroup shape (one launch).
+static hipError_t launch_fdct_fs(const FrameSet<FdctArgs>& fs, hipStream_t s, const KTimer* t) {
+    const FdctArgs& a = fs.a[0];
+    for (uint32_t f = 0; f < fs.n; ++f) {
+        const FdctArgs& m = fs.a[f];
+        // 32-bit buffer offsets: the frame's pixels and coefficients must stay below kOob
+        // (a 16384^2 frame needs 805 MB of each)
+        if ((uint64_t)m.stride * m.g.height >= kOob || (uint64_t)m.g.nblocks() * 128 >= kOob) return hipErrorInvalidValue;
+        if (std::memcmp(&m.g, &a.g, sizeof(Geometry)) != 0 || (m.maxval == 255) != (a.maxval == 255) ||
+            m.solo != a.solo || fs.wg0[f + 1] - fs.wg0[f] != fdct_grid(m.g, m.solo, m.wgs))
+            return hipErrorInvalidValue;
+    }
+    const uint32_t grid = fs.wg0[fs.n];
     // the kernels assume these shapes (kernels.hpp Geometry)
     if (a.g.row8()) {
         switch (a.g.yh) {
             // (launch_timed returns the launch's error: hipGetLastError has already consumed it)
-            case 1: return a.g.bpm != 3 ? hipErrorInvalidValue : launch_row8<1>(a, grid, s, t);
-            case 2: return a.g.bpm != 4 ? hipErrorInvalidValue : launch_row8<2>(a, grid, s, t);
-            case 4: return a.g.bpm != 6 ? hipErrorInvalidValue : launch_row8<4>(a, grid, s, t);
+            case 1: return a.g.bpm != 3 ? hipErrorInvalidValue : launch_row8<1>(fs, grid, s, t);
+            case 2: return a.g.bpm != 4 ? hipErrorInvalidValue : launch_row8<2>(fs, grid, s, t);
+            case 4: return a.g.bpm != 6 ? hipErrorInvalidValue : launch_row8<4>(fs, grid, s, t);
             default: return hipErrorInvalidValue;
         }
     }
     if (a.g.yh != 2 || a.g.bpm != 6) return hipErrorInvalidValue;
     switch (a.g.cfilt) {
-        case kFiltS420m: return launch_420<kFiltS420m>(a, grid, s, t);
-        case kFiltS420lm: return launch_420<kFiltS420lm>(a, grid, s, t);
-        case kFiltS420: return launch_420<kFiltS420>(a, grid, s, t);
+        case kFiltS420m: return launch_420<kFiltS420m>(fs, grid, s, t);
+        case kFiltS420lm: return launch_420<kFiltS420lm>(fs, grid, s, t);
+        case kFiltS420: return launch_420<kFiltS420>(fs, grid, s, t);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
+    return launch_fdct_fs(frame_set(&a, 1, fdct_grid(a.g, a.solo, a.wgs)), s, t);
+}
+
+hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s) {
+    if (n < 1 || n > kMaxSet) return hipErrorInvalidValue;
+    return launch_fdct_fs(frame_set(a, n, fdct_grid(a[0].g, a[0].solo, a[0].wgs)), s, nullptr);
 }
 
 }  // namespace jpge

@@ -357,7 +357,7 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         eq[m] = 0;
         int e = -1;
         for (int k = 1; k < m; ++k) {
-            const bool h = eq[k] & (!(k & 1) | eq[k - 1] | eq[k + 1] | (k >= pe));
+            const bool h = eq[k] & (((k & 1) == 0) | eq[k - 1] | eq[k + 1] | (k >= pe));
             e = h ? k : e;
         }
         return e;

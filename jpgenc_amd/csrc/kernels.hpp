@@ -286,6 +286,38 @@ struct KTimer {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
+// Frames launched together (frame sets): member f of a set owns workgroups
+// [wg0[f], wg0[f + 1]) of one launch and runs exactly as if launched alone with its
+// own arguments and wg0[f + 1] - wg0[f] workgroups.  The members share a geometry
+// (one kernel shape).  Small frames go in sets: a 1080p frame's kernels alone leave
+// most of the GPU idle while their fixed latencies (launch, first loads, last
+// workgroup) pass, so 4 frames per launch do 4 frames' work in about one frame's
+// latency.  Every kernel takes a set; a lone frame is a set of one.
+constexpr int kMaxSet = 4;
+template <typename A>
+struct FrameSet {
+    A a[kMaxSet];
+    uint32_t wg0[kMaxSet + 1];
+    uint32_t n;
+};
+// the member that owns workgroup b (uniform: scalar code)
+JPGE_HD inline uint32_t set_member(const uint32_t* wg0, uint32_t n, uint32_t b) {
+    uint32_t f = 0;
+    for (uint32_t i = 1; i < n; ++i) f += b >= wg0[i] ? 1u : 0u;
+    return f;
+}
+template <typename A>
+inline FrameSet<A> frame_set(const A* a, int n, uint32_t grid_each) {
+    FrameSet<A> s{};
+    s.n = (uint32_t)n;
+    for (int f = 0; f < n; ++f) {
+        s.a[f] = a[f];
+        s.wg0[f] = (uint32_t)f * grid_each;
+    }
+    s.wg0[n] = (uint32_t)n * grid_each;
+    return s;
+}
+
 uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs = 0);
 // statistics workgroups: wgs (0: 3 per CU), within the tile-table bound and the tile count
 uint32_t stats_grid(const SegLayout& L, uint32_t wgs = 0);
@@ -315,6 +347,12 @@ hipError_t launch_huff_tables(const TabArgs& a, uint32_t sets, hipStream_t s);
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t = nullptr);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t = nullptr);
+// frame sets (kMaxSet frames of one geometry, one launch per kernel): the members'
+// arguments as launch_fdct / launch_stats / launch_entropy take them
+hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s);
+hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s);
+// (every member placed by its code kernel's last workgroup: a.done set, no restart)
+hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s);
 // [4][256] summed counts and keys into (mapped) host memory, then *host_seq = seq
 hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
                               uint64_t seq, hipStream_t s);

@@ -112,14 +112,17 @@ struct K2Lds {
 //  D  one lane per non-zero (all lanes busy whatever the block's density): run
 //     (from the block mask), category, symbol, histogram, first-occurrence key, its
 //     record at recbase + 1 + rank + ZRLs; one lane per block: DC and EOB.
-__global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(StatsArgs a) {
+__global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(FrameSet<StatsArgs> fs) {
+    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const StatsArgs& a = fs.a[set_f];
+    const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
     __shared__ K2Lds lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t mw = a.g.mw;
     // the entropy partition's tiles (seg_layout), a contiguous run per workgroup
     const uint32_t ntiles = seg_tiles(a.seg);
-    const uint32_t t_first = (uint32_t)((uint64_t)blockIdx.x * ntiles / gridDim.x);
-    const uint32_t t_last = (uint32_t)((uint64_t)(blockIdx.x + 1) * ntiles / gridDim.x);
+    const uint32_t t_first = (uint32_t)((uint64_t)bid * ntiles / nbk);
+    const uint32_t t_last = (uint32_t)((uint64_t)(bid + 1) * ntiles / nbk);
 #if K2_ZERO128
     // (counters and keys initialised in 16-byte stores: acnt and dcnt are contiguous)
     static_assert((kHistCopies * (kCopyWords + kDcCopyWords)) % 4 == 0 && offsetof(K2Lds, acnt) % 16 == 0 &&
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
     __syncthreads();
     JPGE_STAMP(2);
 
-    const int rep = blockIdx.x % kHistReplicas;
+    const int rep = bid % kHistReplicas;
     const uint64_t ncb = a.key_ncb ? a.key_ncb : a.g.nmcu();  // Cb blocks of the whole image
 #pragma unroll
     for (int r = 0; r < 1024 / kK2Threads; ++r) {
@@ -509,7 +512,10 @@ struct K2WLds {
     uint32_t next;                                       // the next sub-stream to take
 };
 
-__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_WPE))) void stats_wave_kernel(StatsArgs a) {
+__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_WPE))) void stats_wave_kernel(FrameSet<StatsArgs> fs) {
+    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const StatsArgs& a = fs.a[set_f];
+    const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
     __shared__ K2WLds L;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -526,8 +532,8 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
     // the workgroup's sub-streams [s_lo, s_hi) (64-bit divisions lane-parallel, on the VALU)
     uint32_t s_lo, s_hi;
     {
-        const uint32_t w = blockIdx.x + (uint32_t)(lane & 1);
-        const uint32_t v = (uint32_t)((uint64_t)w * S / gridDim.x);
+        const uint32_t w = bid + (uint32_t)(lane & 1);
+        const uint32_t v = (uint32_t)((uint64_t)w * S / nbk);
         s_lo = __builtin_amdgcn_readlane(v, 0);
         s_hi = __builtin_amdgcn_readlane(v, 1);
     }
@@ -752,7 +758,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
     if (K2W_FLUSH == 0) return;
 #endif
 
-    const int rep = blockIdx.x % kHistReplicas;
+    const int rep = bid % kHistReplicas;
     const uint64_t ncb = a.key_ncb ? a.key_ncb : a.g.nmcu();  // Cb blocks of the whole image
     for (int i = tid; i < 1024; i += kWThreads) {
         const uint32_t t = (uint32_t)i >> 8, sy = (uint32_t)i & 255u;
@@ -810,10 +816,13 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     return std::max(std::max(1u, need), std::min(want, cap));
 }
 
-hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
-    // (32-bit block numbers and buffer offsets)
-    if ((uint64_t)a.g.nblocks() * 128 >= (1ull << 32)) return hipErrorInvalidValue;
-    return launch_timed(t, stats_wave_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kWThreads), s, a);
+static hipError_t launch_stats_fs(const FrameSet<StatsArgs>& fs, hipStream_t s, const KTimer* t) {
+    for (uint32_t f = 0; f < fs.n; ++f) {
+        // (32-bit block numbers and buffer offsets)
+        if ((uint64_t)fs.a[f].g.nblocks() * 128 >= (1ull << 32)) return hipErrorInvalidValue;
+        if (fs.wg0[f + 1] - fs.wg0[f] != stats_grid(fs.a[f].seg, fs.a[f].wgs)) return hipErrorInvalidValue;
+    }
+    return launch_timed(t, stats_wave_kernel, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
 }
 #else
 uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
@@ -831,9 +840,20 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     return r < tiles ? r : tiles;
 }
 
-hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
-    return launch_timed(t, stats_kernel, dim3(stats_grid(a.seg, a.wgs)), dim3(kK2Threads), s, a);
+static hipError_t launch_stats_fs(const FrameSet<StatsArgs>& fs, hipStream_t s, const KTimer* t) {
+    for (uint32_t f = 0; f < fs.n; ++f)
+        if (fs.wg0[f + 1] - fs.wg0[f] != stats_grid(fs.a[f].seg, fs.a[f].wgs)) return hipErrorInvalidValue;
+    return launch_timed(t, stats_kernel, dim3(fs.wg0[fs.n]), dim3(kK2Threads), s, fs);
 }
 #endif
+
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
+    return launch_stats_fs(frame_set(&a, 1, stats_grid(a.seg, a.wgs)), s, t);
+}
+
+hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s) {
+    if (n < 1 || n > kMaxSet) return hipErrorInvalidValue;
+    return launch_stats_fs(frame_set(a, n, stats_grid(a[0].seg, a[0].wgs)), s, nullptr);
+}
 
 }  // namespace jpge
