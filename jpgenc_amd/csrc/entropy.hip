@@ -103,8 +103,9 @@ __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, ui
 // every workgroup's WgPlace from the records (the placement scan), kK3Threads threads
 __device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int tid);
 
+template <int kN>
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_WPE))) void entropy_code_kernel(
-    FrameSet<EntropyArgs> fs) {
+    FrameSet<EntropyArgs, kN> fs) {
     __shared__ K3Lds L;
     const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const EntropyArgs& a = fs.a[set_f];
@@ -624,7 +625,8 @@ struct PackLds {
     uint32_t Lb, ftotal, split, fill, seg;
 };
 
-__global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<EntropyArgs> fs) {
+template <int kN>
+__global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<EntropyArgs, kN> fs) {
     __shared__ PackLds S;
     const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const EntropyArgs& a = fs.a[set_f];
@@ -822,7 +824,7 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
 
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tcode, const KTimer* tpack) {
     const uint32_t G = a.seg.grid();
-    hipError_t e = launch_timed(tcode, entropy_code_kernel, dim3(G), dim3(kK3Threads), s, frame_set(&a, 1, G));
+    hipError_t e = launch_timed(tcode, entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&a, 1, G));
     if (e != hipSuccess) return e;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
@@ -834,7 +836,7 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tco
         b.flags |= kExtPlace;
         if ((e = launch_place(b, G, s)) != hipSuccess) return e;
     }
-    return launch_timed(tpack, entropy_pack_kernel, dim3(G), dim3(kK3Threads), s, frame_set(&b, 1, G));
+    return launch_timed(tpack, entropy_pack_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&b, 1, G));
 }
 
 hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s) {
@@ -845,21 +847,21 @@ hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s) {
         const EntropyArgs& m = a[f];
         if (m.seg.grid() != G || !m.done || !m.place || m.rst.mcus || G > kPlaceInCodeMaxWgs) return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(entropy_code_kernel, dim3(G * n), dim3(kK3Threads), 0, s, fs);
+    hipLaunchKernelGGL(entropy_code_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), 0, s, fs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     for (int f = 0; f < n; ++f) {
         fs.a[f].flags |= kExtPlace;
         fs.a[f].dbg = a[f].dbg ? a[f].dbg + 65536 * kStampSlots : nullptr;
     }
-    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G * n), dim3(kK3Threads), 0, s, fs);
+    hipLaunchKernelGGL(entropy_pack_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), 0, s, fs);
     return hipGetLastError();
 }
 
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
     const uint32_t G = a.seg.grid();
     if (!a.summary) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(entropy_code_kernel, dim3(G), dim3(kK3Threads), 0, s, frame_set(&a, 1, G));
+    hipLaunchKernelGGL(entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), 0, s, frame_set<1>(&a, 1, G));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // (restart intervals: the stripe's placement is its own, computed now; its summary
@@ -877,7 +879,7 @@ hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s) {
         const hipError_t e = launch_place(b, G, s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(entropy_pack_kernel, dim3(G), dim3(kK3Threads), 0, s, frame_set(&b, 1, G));
+    hipLaunchKernelGGL(entropy_pack_kernel<1>, dim3(G), dim3(kK3Threads), 0, s, frame_set<1>(&b, 1, G));
     return hipGetLastError();
 }
 

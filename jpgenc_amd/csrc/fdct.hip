@@ -174,8 +174,8 @@ __device__ __forceinline__ void swap_halves(double& a, double& b) {
     b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
 }
 
-template <bool kExact, int kWaves, int kFilt>
-__global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs> fs) {
+template <bool kExact, int kWaves, int kFilt, int kN>
+__global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN> fs) {
     const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const FdctArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
@@ -472,8 +472,8 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs> fs
 constexpr int kRgbPitch444 = 130;  // u32 per staged row of 128 px (+2: even, for uint2 stores)
 static_assert(8 * kRgbPitch444 <= 16 * kRgbPitch, "the 4:4:4 tile fits the 4:2:0 staging area");
 
-template <bool kExact, int kWaves, int kYh>
-__global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArgs> fs) {
+template <bool kExact, int kWaves, int kYh, int kN>
+__global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArgs, kN> fs) {
     const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const FdctArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
@@ -668,29 +668,29 @@ uint32_t k1_tiles(const Geometry& g) {
 }
 bool k1_whole_cu(const Geometry& g, bool solo) { return solo && k1_tiles(g) >= kK1WholeCuTiles; }
 
-template <int kYh>
-hipError_t launch_row8(const FrameSet<FdctArgs>& fs, uint32_t grid, hipStream_t s, const KTimer* t) {
+template <int kYh, int kN>
+hipError_t launch_row8(const FrameSet<FdctArgs, kN>& fs, uint32_t grid, hipStream_t s, const KTimer* t) {
     const FdctArgs& a = fs.a[0];
     const bool ex = a.maxval == 255;
     if (k1_whole_cu(a.g, a.solo)) {
-        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
-        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
+        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesSolo, kYh, kN>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
+        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesSolo, kYh, kN>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
     } else {
-        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
-        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
+        if (ex) return launch_timed(t, fdct_row8_kernel<true, kK1WavesShared, kYh, kN>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
+        else return launch_timed(t, fdct_row8_kernel<false, kK1WavesShared, kYh, kN>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
     }
 }
 
-template <int kFilt>
-hipError_t launch_420(const FrameSet<FdctArgs>& fs, uint32_t grid, hipStream_t s, const KTimer* t) {
+template <int kFilt, int kN>
+hipError_t launch_420(const FrameSet<FdctArgs, kN>& fs, uint32_t grid, hipStream_t s, const KTimer* t) {
     const FdctArgs& a = fs.a[0];
     const bool ex = a.maxval == 255;
     if (k1_whole_cu(a.g, a.solo)) {
-        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
-        else return launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
+        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesSolo, kFilt, kN>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
+        else return launch_timed(t, fdct_kernel<false, kK1WavesSolo, kFilt, kN>, dim3(grid), dim3(kK1WavesSolo * 64), s, fs);
     } else {
-        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
-        else return launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
+        if (ex) return launch_timed(t, fdct_kernel<true, kK1WavesShared, kFilt, kN>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
+        else return launch_timed(t, fdct_kernel<false, kK1WavesShared, kFilt, kN>, dim3(grid), dim3(kK1WavesShared * 64), s, fs);
     }
 }
 
@@ -708,7 +708,8 @@ uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs) {
 }
 
 // A set of frames of one geometry, colour path and workgroup shape (one launch).
-static hipError_t launch_fdct_fs(const FrameSet<FdctArgs>& fs, hipStream_t s, const KTimer* t) {
+template <int kN>
+static hipError_t launch_fdct_fs(const FrameSet<FdctArgs, kN>& fs, hipStream_t s, const KTimer* t) {
     const FdctArgs& a = fs.a[0];
     for (uint32_t f = 0; f < fs.n; ++f) {
         const FdctArgs& m = fs.a[f];
@@ -724,23 +725,23 @@ static hipError_t launch_fdct_fs(const FrameSet<FdctArgs>& fs, hipStream_t s, co
     if (a.g.row8()) {
         switch (a.g.yh) {
             // (launch_timed returns the launch's error: hipGetLastError has already consumed it)
-            case 1: return a.g.bpm != 3 ? hipErrorInvalidValue : launch_row8<1>(fs, grid, s, t);
-            case 2: return a.g.bpm != 4 ? hipErrorInvalidValue : launch_row8<2>(fs, grid, s, t);
-            case 4: return a.g.bpm != 6 ? hipErrorInvalidValue : launch_row8<4>(fs, grid, s, t);
+            case 1: return a.g.bpm != 3 ? hipErrorInvalidValue : launch_row8<1, kN>(fs, grid, s, t);
+            case 2: return a.g.bpm != 4 ? hipErrorInvalidValue : launch_row8<2, kN>(fs, grid, s, t);
+            case 4: return a.g.bpm != 6 ? hipErrorInvalidValue : launch_row8<4, kN>(fs, grid, s, t);
             default: return hipErrorInvalidValue;
         }
     }
     if (a.g.yh != 2 || a.g.bpm != 6) return hipErrorInvalidValue;
     switch (a.g.cfilt) {
-        case kFiltS420m: return launch_420<kFiltS420m>(fs, grid, s, t);
-        case kFiltS420lm: return launch_420<kFiltS420lm>(fs, grid, s, t);
-        case kFiltS420: return launch_420<kFiltS420>(fs, grid, s, t);
+        case kFiltS420m: return launch_420<kFiltS420m, kN>(fs, grid, s, t);
+        case kFiltS420lm: return launch_420<kFiltS420lm, kN>(fs, grid, s, t);
+        case kFiltS420: return launch_420<kFiltS420, kN>(fs, grid, s, t);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
-    return launch_fdct_fs(frame_set(&a, 1, fdct_grid(a.g, a.solo, a.wgs)), s, t);
+    return launch_fdct_fs(frame_set<1>(&a, 1, fdct_grid(a.g, a.solo, a.wgs)), s, t);
 }
 
 hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s) {

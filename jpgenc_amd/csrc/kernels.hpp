@@ -294,10 +294,12 @@ struct KTimer {
 // workgroup) pass, so 4 frames per launch do 4 frames' work in about one frame's
 // latency.  Every kernel takes a set; a lone frame is a set of one.
 constexpr int kMaxSet = 4;
-template <typename A>
+// (N: the kernel instance's capacity; lone frames launch the N = 1 instance, whose
+// kernel arguments are a quarter the size: a launch copies them whole)
+template <typename A, int N = kMaxSet>
 struct FrameSet {
-    A a[kMaxSet];
-    uint32_t wg0[kMaxSet + 1];
+    A a[N];
+    uint32_t wg0[N + 1];
     uint32_t n;
 };
 // the member that owns workgroup b (uniform: scalar code)
@@ -306,9 +308,9 @@ JPGE_HD inline uint32_t set_member(const uint32_t* wg0, uint32_t n, uint32_t b) 
     for (uint32_t i = 1; i < n; ++i) f += b >= wg0[i] ? 1u : 0u;
     return f;
 }
-template <typename A>
-inline FrameSet<A> frame_set(const A* a, int n, uint32_t grid_each) {
-    FrameSet<A> s{};
+template <int N = kMaxSet, typename A>
+inline FrameSet<A, N> frame_set(const A* a, int n, uint32_t grid_each) {
+    FrameSet<A, N> s{};
     s.n = (uint32_t)n;
     for (int f = 0; f < n; ++f) {
         s.a[f] = a[f];

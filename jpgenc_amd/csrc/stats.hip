@@ -112,7 +112,8 @@ struct K2Lds {
 //  D  one lane per non-zero (all lanes busy whatever the block's density): run
 //     (from the block mask), category, symbol, histogram, first-occurrence key, its
 //     record at recbase + 1 + rank + ZRLs; one lane per block: DC and EOB.
-__global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(FrameSet<StatsArgs> fs) {
+template <int kN>
+__global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(FrameSet<StatsArgs, kN> fs) {
     const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const StatsArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
@@ -512,7 +513,8 @@ struct K2WLds {
     uint32_t next;                                       // the next sub-stream to take
 };
 
-__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_WPE))) void stats_wave_kernel(FrameSet<StatsArgs> fs) {
+template <int kN>
+__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_WPE))) void stats_wave_kernel(FrameSet<StatsArgs, kN> fs) {
     const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const StatsArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
@@ -816,13 +818,14 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     return std::max(std::max(1u, need), std::min(want, cap));
 }
 
-static hipError_t launch_stats_fs(const FrameSet<StatsArgs>& fs, hipStream_t s, const KTimer* t) {
+template <int kN>
+static hipError_t launch_stats_fs(const FrameSet<StatsArgs, kN>& fs, hipStream_t s, const KTimer* t) {
     for (uint32_t f = 0; f < fs.n; ++f) {
         // (32-bit block numbers and buffer offsets)
         if ((uint64_t)fs.a[f].g.nblocks() * 128 >= (1ull << 32)) return hipErrorInvalidValue;
         if (fs.wg0[f + 1] - fs.wg0[f] != stats_grid(fs.a[f].seg, fs.a[f].wgs)) return hipErrorInvalidValue;
     }
-    return launch_timed(t, stats_wave_kernel, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
+    return launch_timed(t, stats_wave_kernel<kN>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
 }
 #else
 uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
@@ -840,15 +843,16 @@ uint32_t stats_grid(const SegLayout& L, uint32_t wgs) {
     return r < tiles ? r : tiles;
 }
 
-static hipError_t launch_stats_fs(const FrameSet<StatsArgs>& fs, hipStream_t s, const KTimer* t) {
+template <int kN>
+static hipError_t launch_stats_fs(const FrameSet<StatsArgs, kN>& fs, hipStream_t s, const KTimer* t) {
     for (uint32_t f = 0; f < fs.n; ++f)
         if (fs.wg0[f + 1] - fs.wg0[f] != stats_grid(fs.a[f].seg, fs.a[f].wgs)) return hipErrorInvalidValue;
-    return launch_timed(t, stats_kernel, dim3(fs.wg0[fs.n]), dim3(kK2Threads), s, fs);
+    return launch_timed(t, stats_kernel<kN>, dim3(fs.wg0[fs.n]), dim3(kK2Threads), s, fs);
 }
 #endif
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
-    return launch_stats_fs(frame_set(&a, 1, stats_grid(a.seg, a.wgs)), s, t);
+    return launch_stats_fs(frame_set<1>(&a, 1, stats_grid(a.seg, a.wgs)), s, t);
 }
 
 hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s) {
