@@ -162,6 +162,7 @@ constexpr int kMaxDrainLag = 4;
 constexpr int kMaxTableThreads = 16;
 constexpr int kMaxLanes = 8;
 constexpr uint64_t kInlineTablesMinPixels = 4u << 20;  // frames this large build their tables on the lane thread
+constexpr uint64_t kFirstSleepMaxPixels = 16u << 20;   // frames this large poll their results without a first sleep
 
 double abs_us(std::chrono::steady_clock::time_point t) {  // host-trace clock
     return std::chrono::duration<double, std::micro>(t.time_since_epoch()).count();
@@ -331,6 +332,7 @@ struct Encoder::Slot {
     uint64_t symbols = 0;              // Huffman-coded symbols (= K2 symbol records) of the frame
     uint8_t qy[64], qc[64];
     bool timed = false;                // this frame's kernels are bracketed by timing events
+    int timed_frames = 1;              // frames those kernels covered (a frame set's launches)
     HistPtrs hist{};                   // this frame's device histograms (in d_ctl)
     uint64_t seq = 0;                  // frame sequence number (handshakes via mapped memory)
     std::atomic<int> tables_done{0};   // set by build_tables (any thread)
@@ -464,6 +466,8 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->inline_tables_ = env_int("JPGE_INLINE_TABLES", 2, 0, 2);
     e->nap_us_ = env_int("JPGE_NAP_US", e->nap_us_, 1, 1000);
     e->first_sleep_ = env_int("JPGE_FIRST_SLEEP", (int)(e->first_sleep_ * 100 + 0.5), 0, 95) / 100.0;
+    // (the table pool sleeps first only when asked: the 1080p batch lost 9% to it)
+    e->pool_first_sleep_ = std::getenv("JPGE_FIRST_SLEEP") ? e->first_sleep_ : 0.0;
     const int nap = env_int("JPGE_NAP", -1, -1, 1);
     e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
     e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
@@ -786,6 +790,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     StatsArgs st2;
     if (const int st = prep1(s, f, qy, qc, flags, imp, a, st2)) return st;
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
+    s.timed_frames = 1;
     // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
     const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
     JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
@@ -805,9 +810,16 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
 // are not in the set).  Their histograms leave through a later code kernel or
 // launch_hist_export.
 int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a, const StatsArgs* st) {
-    for (int m = 0; m < n; ++m) s[m]->timed = false;  // (no per-frame kernel events in a set)
-    JPGE_HIP(launch_fdct_set(a, n, s[0]->stream));
-    JPGE_HIP(launch_stats_set(st, n, s[0]->stream));
+    // a sampled set: its launches timed with the first member's events, as n frames' work
+    for (int m = 0; m < n; ++m) s[m]->timed = false;
+    const uint64_t c = frame_counter_.fetch_add((uint64_t)n);
+    Slot& t = *s[0];
+    const uint64_t E = (uint64_t)timing_every_;
+    t.timed = E && (c + E - 1) / E * E <= c + (uint64_t)n - 1;  // (a sampled frame number in the set)
+    t.timed_frames = n;
+    const KTimer t1{t.ev[0], t.ev[1]}, t2{t.ev[2], t.ev[3]};
+    JPGE_HIP(launch_fdct_set(a, n, t.stream, t.timed ? &t1 : nullptr));
+    JPGE_HIP(launch_stats_set(st, n, t.stream, t.timed ? &t2 : nullptr));
     for (int m = 0; m < n; ++m) {
         s[m]->seq = ++seq_counter_;
         s[m]->hist = st[m].hist;
@@ -916,7 +928,10 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
 }
 
 int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
-    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, s.guess_result)) return w;
+    // (a first sleep only up to kFirstSleepMaxPixels: 16384^2 frames, few per lane and
+    // irregular, lost 3.7% to it)
+    WaitGuess* const guess = (uint64_t)s.g.width * s.g.height <= kFirstSleepMaxPixels ? s.guess_result : nullptr;
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, guess)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[7]));
         std::lock_guard<std::mutex> g(times_mu_);
@@ -932,8 +947,8 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
         times_.entropy_sum += times_.entropy;
         times_.code_sum += code;
         times_.pack_sum += pack;
-        times_.frames += 1;
-        times_.symbols += s.symbols;
+        times_.frames += s.timed_frames;                       // (the launches' frames)
+        times_.symbols += s.symbols * (uint64_t)s.timed_frames;  // (a set: its first member's, for each)
     }
     if (stamps_file_) hipStreamSynchronize(s.stream);
     dump_stamps(s);
@@ -972,7 +987,7 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
-    if (inline_tables_ != 1 && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_, first_sleep_));
+    if (inline_tables_ != 1 && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_, pool_first_sleep_));
     // Frames are dealt dynamically: a lane takes the batch's next frame (or frame set)
     // when its pipeline has room, so lanes finish together.  Lane 0 runs on the calling
     // thread.
@@ -1014,10 +1029,12 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     return st;
 }
 
-// Frames per launch: sets of frames of one small geometry (kernels.hpp FrameSet), about
-// a 4K frame's pixels per launch.  A set's entropy launch needs every member placed by
-// its own last code workgroup (the pipeline's placement mode, no restart intervals).
-constexpr uint64_t kSetPixels = 3840ull * 2160ull;
+// Frames per launch: sets of frames of one geometry (kernels.hpp FrameSet), up to
+// kMaxSet and about four 4K frames' pixels per launch (4K: 192 -> 208 GPix/s with sets
+// of 4, 203 with 2; 1080p batch: 111 -> 143).  A set's entropy launch needs every member
+// placed by its own last code workgroup (the pipeline's placement mode, no restart
+// intervals).
+constexpr uint64_t kSetPixels = 4ull * 3840ull * 2160ull;
 int Encoder::batch_set_size(const FrameDesc* fr, int n) const {
     if (n < 2 || set_ == 1) return 1;
     const FrameDesc& f0 = fr[0];
@@ -1226,8 +1243,15 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
             }
             if (ne) {
                 if (as_set) {
-                    for (int q = 0; q < ne; ++q) sj[ms[q]]->h_result[2] = 0;
-                    const hipError_t e = launch_entropy_set(ea, ne, sj[ms[0]]->stream);
+                    Slot* tm = nullptr;  // (a sampled set's member: its events time the launches)
+                    for (int q = 0; q < ne; ++q) {
+                        sj[ms[q]]->h_result[2] = 0;
+                        if (sj[ms[q]]->timed && !tm) tm = sj[ms[q]];
+                    }
+                    const KTimer tc{tm ? tm->ev[4] : nullptr, tm ? tm->ev[5] : nullptr};
+                    const KTimer tp{tm ? tm->ev[6] : nullptr, tm ? tm->ev[7] : nullptr};
+                    const hipError_t e = launch_entropy_set(ea, ne, sj[ms[0]]->stream, tm ? &tc : nullptr,
+                                                            tm ? &tp : nullptr);
                     for (int q = 0; q < ne; ++q) note(j, ms[q], e == hipSuccess ? kOk : kErrHip);
                     if (e != hipSuccess) ne = 0;
                 } else {

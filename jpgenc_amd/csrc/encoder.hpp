@@ -186,10 +186,11 @@ class Encoder {
     int inline_tables_ = 2;     // JPGE_INLINE_TABLES: 1 each lane's thread builds its frames' tables, 0 the
                                 // pool, 2 (default) by frame size (encoder.cpp kInlineTablesMinPixels)
     int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
-    // JPGE_FIRST_SLEEP (percent, default off): a lane's first sleep in a wait, of its usual
-    // length.  At 70%: 4K host CPU 1.8 -> 1.7 at equal throughput, but 16384^2 frames (4 per
-    // lane per batch, irregular waits) lost 14% to oversleeping.
-    double first_sleep_ = 0;
+    // JPGE_FIRST_SLEEP (percent): a lane's first sleep in a result wait, of its usual length
+    // less twice its spread (WaitGuess).  At 80%: 4K host CPU 1.45 -> 1.22 at equal
+    // throughput; frames above kFirstSleepMaxPixels (16384^2: -3.7%) poll without it.
+    double first_sleep_ = 0.8;
+    double pool_first_sleep_ = 0;  // the table pool's (JPGE_FIRST_SLEEP given: the same)
     // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
     // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
     // lanes (one small launch instead of every pack workgroup scanning all records:

@@ -839,7 +839,7 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tco
     return launch_timed(tpack, entropy_pack_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&b, 1, G));
 }
 
-hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s) {
+hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s, const KTimer* tcode, const KTimer* tpack) {
     if (n < 1 || n > kMaxSet) return hipErrorInvalidValue;
     const uint32_t G = a[0].seg.grid();
     FrameSet<EntropyArgs> fs = frame_set(a, n, G);
@@ -847,15 +847,13 @@ hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s) {
         const EntropyArgs& m = a[f];
         if (m.seg.grid() != G || !m.done || !m.place || m.rst.mcus || G > kPlaceInCodeMaxWgs) return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(entropy_code_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), 0, s, fs);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_timed(tcode, entropy_code_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), s, fs);
     if (e != hipSuccess) return e;
     for (int f = 0; f < n; ++f) {
         fs.a[f].flags |= kExtPlace;
         fs.a[f].dbg = a[f].dbg ? a[f].dbg + 65536 * kStampSlots : nullptr;
     }
-    hipLaunchKernelGGL(entropy_pack_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), 0, s, fs);
-    return hipGetLastError();
+    return launch_timed(tpack, entropy_pack_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), s, fs);
 }
 
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {

@@ -744,9 +744,9 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t) {
     return launch_fdct_fs(frame_set<1>(&a, 1, fdct_grid(a.g, a.solo, a.wgs)), s, t);
 }
 
-hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s) {
+hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s, const KTimer* t) {
     if (n < 1 || n > kMaxSet) return hipErrorInvalidValue;
-    return launch_fdct_fs(frame_set(a, n, fdct_grid(a[0].g, a[0].solo, a[0].wgs)), s, nullptr);
+    return launch_fdct_fs(frame_set(a, n, fdct_grid(a[0].g, a[0].solo, a[0].wgs)), s, t);
 }
 
 }  // namespace jpge

@@ -351,10 +351,11 @@ hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t = nullp
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t = nullptr);
 // frame sets (kMaxSet frames of one geometry, one launch per kernel): the members'
 // arguments as launch_fdct / launch_stats / launch_entropy take them
-hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s);
-hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s);
+hipError_t launch_fdct_set(const FdctArgs* a, int n, hipStream_t s, const KTimer* t = nullptr);
+hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s, const KTimer* t = nullptr);
 // (every member placed by its code kernel's last workgroup: a.done set, no restart)
-hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s);
+hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s, const KTimer* code = nullptr,
+                              const KTimer* pack = nullptr);
 // [4][256] summed counts and keys into (mapped) host memory, then *host_seq = seq
 hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* host_key, uint64_t* host_seq,
                               uint64_t seq, hipStream_t s);

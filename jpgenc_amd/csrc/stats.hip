@@ -855,9 +855,9 @@ hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
     return launch_stats_fs(frame_set<1>(&a, 1, stats_grid(a.seg, a.wgs)), s, t);
 }
 
-hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s) {
+hipError_t launch_stats_set(const StatsArgs* a, int n, hipStream_t s, const KTimer* t) {
     if (n < 1 || n > kMaxSet) return hipErrorInvalidValue;
-    return launch_stats_fs(frame_set(a, n, stats_grid(a[0].seg, a[0].wgs)), s, nullptr);
+    return launch_stats_fs(frame_set(a, n, stats_grid(a[0].seg, a[0].wgs)), s, t);
 }
 
 }  // namespace jpge
