@@ -733,10 +733,26 @@ def run_frames(args, rank, local, world, pg):
     # Solo pass (after the timed region, not part of `value`): the distinct frames
     # through a single-lane encoder with events around every frame's kernels, so each
     # kernel's duration is its own, without other lanes' kernels beside it.
-    tm_solo = None
-    solo_win = None
-    if args.solo_batches > 0 and not args.no_kernel_events:
-        solo = J.Encoder(local, lanes=1)
+    # Two solo passes: launches as the pipeline makes them (frame sets of `set_size`
+    # frames, encoder.cpp batch_set_size; the headline roofline) and one frame per launch.
+    tm_solo = tm_solo1 = None
+    solo_win = solo1_win = None
+    set_size = max(1, min(4, (4 * 3840 * 2160) // (W * H))) if D >= 2 else 1
+
+    def solo_pass(fset):
+        env = {"JPGE_SET": str(fset)}
+        if fset > 1:  # (a 1-lane encoder places by the pack kernels unless told otherwise; sets place in the code kernel)
+            env["JPGE_EXT_PLACE"] = "1"
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            solo = J.Encoder(local, lanes=1)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         solo.set_subsampling(args.subsampling)
         sfr, sout = frames[:D], outd[:D]
         # warm-up batches first (~20 ms at 4K): right after the 4-lane region the chip's
@@ -748,9 +764,14 @@ def run_frames(args, rank, local, world, pg):
         s0 = time.monotonic_ns()
         for _ in range(args.solo_batches):
             solo.encode_batch_dev(sfr, sout, quality=args.quality)
-        solo_win = [s0, time.monotonic_ns()]
-        tm_solo = solo.timing()
+        win = [s0, time.monotonic_ns()]
+        tm = solo.timing()
         solo.close()
+        return tm, win
+
+    if args.solo_batches > 0 and not args.no_kernel_events:
+        tm_solo, solo_win = solo_pass(set_size)
+        tm_solo1, solo1_win = solo_pass(1) if set_size > 1 else (tm_solo, solo_win)
 
     # per-kernel rooflines (HBM-bound integer/fp64 work; algorithmic bytes per launch)
     npx = W * H
@@ -774,26 +795,32 @@ def run_frames(args, rank, local, world, pg):
     pmc_key = {"entropy_stage": "entropy_kernel"}
 
     def rooflines(tm):
-        nfr = max(1, tm["frames"])
+        # per launch: a frame set's launch covers frames_per_launch frames (its bytes and
+        # its duration both); traffic (PMC, profiles/) is per frame
+        nl = max(1, tm.get("launches") or tm["frames"])
+        fpl = tm["frames"] / nl if tm["frames"] else 1.0
         out = {}
         for name, (b, what) in list(alg.items()) + list(stage_alg.items()):
-            ms = tm[tm_key[name]] / nfr
-            ach = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # (0: --no-kernel-events)
+            ms = tm[tm_key[name]] / nl
+            bl = b * fpl
+            ach = bl / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # (0: --no-kernel-events)
+            tr = traffic.get(pmc_key.get(name, name))
             out[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic.get(pmc_key.get(name, name)),
-                         "alg_bytes_per_launch": int(b), "alg_bytes": what, "avg_kernel_ms": round(ms, 5),
-                         "timed_launches": tm["frames"]}
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(tr * fpl) if tr else tr,
+                         "alg_bytes_per_launch": int(bl), "alg_bytes": what, "avg_kernel_ms": round(ms, 5),
+                         "timed_launches": nl, "frames_per_launch": round(fpl, 3)}
         # the north star's "HBM-read roofline": K1's RGB8 read alone (3 B/px)
         k1 = out["fdct_kernel"]
-        ms1 = tm["fdct_sum"] / nfr
+        ms1 = tm["fdct_sum"] / nl
         if ms1 > 0:
-            rd = 3.0 * npx / (ms1 * 1e-3) / 1e9
+            rd = 3.0 * npx * fpl / (ms1 * 1e-3) / 1e9
             k1["read_achieved"] = round(rd, 1)
             k1["read_frac"] = round(rd / HBM_PEAK_GBS, 4)
         return out
 
     stages = rooflines(tm)  # in situ: the timed region, lanes side by side (overlapping: diagnostic)
     stages_solo = rooflines(tm_solo) if tm_solo else None
+    stages_solo1 = rooflines(tm_solo1) if tm_solo1 else None
     ms_step = dt_max / args.steps * 1e3
     # The headline roofline: the dominant kernel (longest exclusive time) ALONE on the GPU
     # (the solo pass), its duration from events bound to its own dispatch, so the figure
@@ -805,11 +832,12 @@ def run_frames(args, rank, local, world, pg):
         roofline = dict(kernel=dominant, timing="solo (1-lane encoder after the timed region; HIP events bound "
                                                 "to the kernel's dispatch, hipExtLaunchKernel)", **stages_solo[dominant])
         # exclusive time of one launch x launches per step cannot exceed the step
-        spent = F * roofline["avg_kernel_ms"]
-        roofline["check"] = {"launches_per_step": F, "launches_x_avg_ms": round(spent, 3),
+        lps = F / roofline["frames_per_launch"]
+        spent = lps * roofline["avg_kernel_ms"]
+        roofline["check"] = {"launches_per_step": round(lps, 1), "launches_x_avg_ms": round(spent, 3),
                              "ms_per_step": round(ms_step, 3), "ok": spent <= ms_step}
         if spent > ms_step:
-            raise SystemExit(f"bench: roofline check failed: {F} launches x {roofline['avg_kernel_ms']} ms "
+            raise SystemExit(f"bench: roofline check failed: {lps:.1f} launches x {roofline['avg_kernel_ms']} ms "
                              f"= {spent:.3f} ms > {ms_step:.3f} ms per step")
     elif stages["fdct_kernel"]["avg_kernel_ms"] > 0:
         # no solo pass (--solo-batches 0): the in-situ figure, labelled as such (lanes
@@ -855,18 +883,21 @@ def run_frames(args, rank, local, world, pg):
             "roofline_pipeline": pipeline,
             "stages": stages,
             "stages_solo": stages_solo,
-            "kernel_events": f"each kernel of a sampled frame launched with its own HIP events bound to its "
-                             f"dispatch (hipExtLaunchKernel). stages: in situ, every {args.event_every}th frame in "
-                             f"the timed region (4 lanes overlap: a diagnostic, not exclusive time); stages_solo: "
-                             f"every frame of {args.solo_batches} batches of {D} on a 1-lane encoder after the "
-                             f"timed region",
+            "stages_solo_single_frame": stages_solo1,
+            "kernel_events": f"each kernel launch of a sampled frame (set) launched with its own HIP events bound "
+                             f"to its dispatch (hipExtLaunchKernel); figures per launch, a frame set's launch "
+                             f"covering frames_per_launch frames. stages: in situ, the set of every "
+                             f"{args.event_every}th frame in the timed region (4 lanes overlap: a diagnostic, not "
+                             f"exclusive time); stages_solo: every launch of {args.solo_batches} batches of {D} on a "
+                             f"1-lane encoder after the timed region, in the pipeline's frame sets of {set_size}; "
+                             f"stages_solo_single_frame: the same, one frame per launch",
             "step_ms": {"min": round(min(step_t) * 1e3, 3), "median": round(sorted(step_t)[len(step_t) // 2] * 1e3, 3),
                         "max": round(max(step_t) * 1e3, 3)},
             "lanes": enc.lanes(),
             "verified": verified,
             "d2h": d2h,
             # CLOCK_MONOTONIC windows (rocprofv3 timestamps use the same clock): tools/rocprof_window.py
-            "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win},
+            "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win, "solo_single": solo1_win},
             # host CPU use over the timed region; quota throttling stalls the pipeline
             "host_cpu": host_cpu_use(cg0, cg1, dt),
             "devices": args.devices,

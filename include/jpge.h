@@ -67,6 +67,8 @@ typedef struct {
     uint64_t frames;                            /* frames accumulated */
     uint64_t symbols; /* Huffman-coded symbols of those frames (= K2's 4-byte symbol records) */
     double code_sum, pack_sum; /* K3's entropy_code_kernel and entropy_pack_kernel alone (ms, accumulated) */
+    uint64_t launches;         /* timed launches of each kernel (batches of small frames launch frame sets:
+                                  one launch per kernel for up to 4 frames; the sums are per launch) */
 } jpge_timing;
 
 const char* jpge_strerror(int status);

@@ -98,7 +98,8 @@ class Timing(ctypes.Structure):
     _fields_ = [("fdct", ctypes.c_float), ("dc_stats", ctypes.c_float), ("entropy", ctypes.c_float),
                 ("total", ctypes.c_float), ("fdct_sum", ctypes.c_double), ("dc_stats_sum", ctypes.c_double),
                 ("entropy_sum", ctypes.c_double), ("frames", ctypes.c_uint64),
-                ("symbols", ctypes.c_uint64), ("code_sum", ctypes.c_double), ("pack_sum", ctypes.c_double)]
+                ("symbols", ctypes.c_uint64), ("code_sum", ctypes.c_double), ("pack_sum", ctypes.c_double),
+                ("launches", ctypes.c_uint64)]
 
 
 _LIB = None
@@ -451,7 +452,8 @@ class Encoder:
         _check(lib().jpge_get_timing(self._ctx, ctypes.byref(t)), "get_timing")
         return {"fdct": t.fdct, "dc_stats": t.dc_stats, "entropy": t.entropy, "total": t.total,
                 "fdct_sum": t.fdct_sum, "dc_stats_sum": t.dc_stats_sum, "entropy_sum": t.entropy_sum,
-                "frames": t.frames, "symbols": t.symbols, "code_sum": t.code_sum, "pack_sum": t.pack_sum}
+                "frames": t.frames, "symbols": t.symbols, "code_sum": t.code_sum, "pack_sum": t.pack_sum,
+                "launches": t.launches}
 
     def reset_timing(self) -> None:
         _check(lib().jpge_reset_timing(self._ctx), "reset_timing")

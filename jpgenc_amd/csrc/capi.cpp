@@ -178,6 +178,7 @@ int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
     t->symbols = k.symbols;
     t->code_sum = k.code_sum;
     t->pack_sum = k.pack_sum;
+    t->launches = k.launches;
     return JPGE_OK;
 }
 

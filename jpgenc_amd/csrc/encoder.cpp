@@ -948,6 +948,7 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
         times_.code_sum += code;
         times_.pack_sum += pack;
         times_.frames += s.timed_frames;                       // (the launches' frames)
+        times_.launches += 1;
         times_.symbols += s.symbols * (uint64_t)s.timed_frames;  // (a set: its first member's, for each)
     }
     if (stamps_file_) hipStreamSynchronize(s.stream);

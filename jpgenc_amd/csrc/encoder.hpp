@@ -41,6 +41,7 @@ struct KernelTimes {  // milliseconds of the last timed frame (each kernel's own
     uint64_t frames = 0;
     uint64_t symbols = 0;  // Huffman-coded symbols of the timed frames
     double code_sum = 0, pack_sum = 0;  // the entropy stage's code and pack kernels alone
+    uint64_t launches = 0;  // timed launches of each kernel (a frame set's launch covers its frames)
 };
 
 class Encoder {

@@ -28,7 +28,7 @@ def main():
     for f in glob.glob(f"{tdir}/**/*kernel_trace.csv*", recursive=True):
         for r in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
             ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
-    for label in ("timed", "solo"):
+    for label in ("timed", "solo", "solo_single"):
         w = wins.get(label)
         if not w:
             continue
@@ -39,12 +39,13 @@ def main():
         print(f"{label} window ({(w[1] - w[0]) / 1e6:.2f} ms):")
         for n, v in sorted(d.items(), key=lambda x: -sum(x[1])):
             extra = ""
-            if label == "solo" and len(v) >= 64:  # the solo pass's batches of 32 frames
+            if label == "solo_single" and len(v) >= 64:  # the single-frame pass's batches of 32 frames
                 extra = " (batches: " + " ".join(f"{sum(v[i:i + 32]) / len(v[i:i + 32]) / 1e3:.2f}"
                                                  for i in range(0, len(v), 32)) + ")"
             print(f"   {n:28s} n={len(v):5d} mean {sum(v) / len(v) / 1e3:8.2f} us  median "
                   f"{statistics.median(v) / 1e3:8.2f} us{extra}")
-        ev = b["stages"] if label == "timed" else b.get("stages_solo") or {}
+        ev = {"timed": b["stages"], "solo": b.get("stages_solo"),
+              "solo_single": b.get("stages_solo_single_frame")}[label] or {}
         for k, v in ev.items():
             print(f"   bench HIP events {k:18s} {v['avg_kernel_ms'] * 1e3:8.2f} us "
                   f"(entropy = code + pack launches)")
