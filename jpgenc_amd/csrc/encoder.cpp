@@ -105,11 +105,8 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int 
     clk::time_point idle_since{};  // the stream was first seen idle without the word
     bool idle = false;
     if (guess) ++guess->waits;
-    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
-        if (guess) {
-            guess->ema_us *= 0.85;
-            ++guess->ready;
-        }
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {  // (not a wait: the estimate is of waits)
+        if (guess) ++guess->ready;
         return kOk;
     }
     if (nap && guess && guess->frac > 0 && guess->first_sleep_us() > 3.0 * nap_us) {
@@ -927,10 +924,13 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
     return kOk;
 }
 
-int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags) {
+int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait) {
     // (a first sleep only up to kFirstSleepMaxPixels: 16384^2 frames, few per lane and
     // irregular, lost 3.7% to it)
-    WaitGuess* const guess = (uint64_t)s.g.width * s.g.height <= kFirstSleepMaxPixels ? s.guess_result : nullptr;
+    // (a set's later members: their results follow the first one's within microseconds,
+    // and their short waits would blur the estimate of the real one)
+    WaitGuess* const guess =
+        guess_wait && (uint64_t)s.g.width * s.g.height <= kFirstSleepMaxPixels ? s.guess_result : nullptr;
     if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, guess)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[7]));
@@ -1284,7 +1284,7 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         if (k >= 0 && k < n) {
             for (int m = 0; m < members(k); ++m) {
                 Slot& s = slot(k, m);
-                if (!frame(k, m).status) note(k, m, finish(s, frame(k, m), flags));
+                if (!frame(k, m).status) note(k, m, finish(s, frame(k, m), flags, /*guess_wait=*/m == 0));
                 else hipStreamSynchronize(s.stream);
             }
         }

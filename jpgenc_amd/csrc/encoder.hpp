@@ -151,7 +151,7 @@ class Encoder {
     // phase 2b (GPU): table upload (when not carried) + entropy kernels
     int import_tables_copy(Slot& s);
     int launch_entropy_phase(Slot& s, Slot* exp);
-    int finish(Slot& s, FrameDesc& f, uint32_t flags);
+    int finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait = true);
     // one lane's software pipeline over the frames it takes from fr[0..total) through `next`
     // (frames go in sets of `set` when set > 1: a pipeline step is a set, one launch per kernel)
     int run_lane(Lane& ln, FrameDesc* fr, int total, std::atomic<int>* next, int set, const uint8_t qy[64],

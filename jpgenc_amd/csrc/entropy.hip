@@ -107,7 +107,7 @@ template <int kN>
 __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_WPE))) void entropy_code_kernel(
     FrameSet<EntropyArgs, kN> fs) {
     __shared__ K3Lds L;
-    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const EntropyArgs& a = fs.a[set_f];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t wg = blockIdx.x - fs.wg0[set_f], G = fs.wg0[set_f + 1] - fs.wg0[set_f];
@@ -628,7 +628,7 @@ struct PackLds {
 template <int kN>
 __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<EntropyArgs, kN> fs) {
     __shared__ PackLds S;
-    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const EntropyArgs& a = fs.a[set_f];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t wg = blockIdx.x - fs.wg0[set_f], G = fs.wg0[set_f + 1] - fs.wg0[set_f];

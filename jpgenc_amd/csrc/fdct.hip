@@ -176,9 +176,16 @@ __device__ __forceinline__ void swap_halves(double& a, double& b) {
 
 template <bool kExact, int kWaves, int kFilt, int kN>
 __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN> fs) {
-    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const FdctArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
+    // the arguments the tile loop reads, loaded once into scalar registers: a set
+    // member's arguments sit at a computed kernarg offset, and the compiler otherwise
+    // reloads them per tile (scalar loads whose lgkmcnt waits also wait for LDS traffic)
+    const uint8_t* rgb_ = a.rgb;
+    uint64_t stride_ = a.stride;
+    uint32_t gw_ = a.g.width, gh_ = a.g.height;
+    asm volatile("" : "+s"(rgb_), "+s"(stride_), "+s"(gw_), "+s"(gh_));
     constexpr int kK1Threads = kWaves * 64;
     __shared__ K1Lds<kWaves> lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;  // wv: 0..15
@@ -188,7 +195,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
     const uint32_t tiles_per_row = (mw + 3) / 4;
     const uint32_t ntiles = tiles_per_row * a.g.mh;
     const double scale = 255.0 / (double)a.maxval;  // Image.cpp:465
-    const bool aligned = (((uintptr_t)a.rgb | a.stride) & 15) == 0;
+    const bool aligned = (((uintptr_t)rgb_ | stride_) & 15) == 0;
     const int r16 = lane >> 2, c16 = lane & 3;  // staging: lane -> (pixel row, 16-px chunk)
     const int b8 = lane >> 3, j = lane & 7;     // DCT: lane -> (block of the round, column)
 
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
     // issues the same 3 loads and 3 stores with no branch around them, and the
     // wait for the prefetched pixels leaves the previous tile's stores in flight.
     const __amdgpu_buffer_rsrc_t rgb_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.rgb), 0, (int)(uint32_t)((uint64_t)a.stride * (a.g.height - 1) + 3ull * a.g.width),
+        const_cast<uint8_t*>(rgb_), 0, (int)(uint32_t)((uint64_t)stride_ * (gh_ - 1) + 3ull * gw_),
         0x00020000);
     const __amdgpu_buffer_rsrc_t coef_rs =
         __builtin_amdgcn_make_buffer_rsrc(a.coef, 0, (int)(uint32_t)((uint64_t)a.g.nblocks() * 128), 0x00020000);
@@ -219,13 +226,13 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
     // fast path (else zeros, and the staging takes the clamped edge path)
     // (tile numbers are wave-uniform: the tile's row and column come from scalar
     // arithmetic, and only this lane's fixed offset within the tile is per lane)
-    const uint32_t lane_off = (uint32_t)r16 * (uint32_t)a.stride + (uint32_t)c16 * 48u;
+    const uint32_t lane_off = (uint32_t)r16 * (uint32_t)stride_ + (uint32_t)c16 * 48u;
     auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
         const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * 4;
         const uint32_t y = mrow * 16 + r16, xs = mcol0 * 16 + c16 * 16;
-        const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
-        const uint32_t base = (uint32_t)((uint64_t)(mrow * 16) * a.stride + (uint64_t)mcol0 * 48);  // (uniform)
+        const bool ok = k < n_p && aligned && y < gh_ && xs + 16 <= gw_;
+        const uint32_t base = (uint32_t)((uint64_t)(mrow * 16) * stride_ + (uint64_t)mcol0 * 48);  // (uniform)
         const uint32_t off = ok ? base + lane_off : kOob;
         v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
         v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
@@ -379,10 +386,10 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
             }
         }
         if (!cfast) {  // right/bottom edge replication (Image.cpp:498-531) as clamped addressing
-            const uint32_t sy = min(y, a.g.height - 1);
+            const uint32_t sy = min(y, gh_ - 1);
             for (int i = 0; i < 16; ++i) {
-                const uint32_t sx = min(xs + i, a.g.width - 1);
-                const uint8_t* p = a.rgb + (uint64_t)sy * a.stride + (uint64_t)sx * 3;
+                const uint32_t sx = min(xs + i, gw_ - 1);
+                const uint8_t* p = rgb_ + (uint64_t)sy * stride_ + (uint64_t)sx * 3;
                 px[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
             }
         }
@@ -474,9 +481,16 @@ static_assert(8 * kRgbPitch444 <= 16 * kRgbPitch, "the 4:4:4 tile fits the 4:2:0
 
 template <bool kExact, int kWaves, int kYh, int kN>
 __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArgs, kN> fs) {
-    const uint32_t set_f = set_member(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
     const FdctArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
+    // the arguments the tile loop reads, loaded once into scalar registers: a set
+    // member's arguments sit at a computed kernarg offset, and the compiler otherwise
+    // reloads them per tile (scalar loads whose lgkmcnt waits also wait for LDS traffic)
+    const uint8_t* rgb_ = a.rgb;
+    uint64_t stride_ = a.stride;
+    uint32_t gw_ = a.g.width, gh_ = a.g.height;
+    asm volatile("" : "+s"(rgb_), "+s"(stride_), "+s"(gw_), "+s"(gh_));
     constexpr int kK1Threads = kWaves * 64;
     constexpr uint32_t kMcus = 16 / kYh;            // MCUs per tile
     constexpr int kBpm = kYh + 2;                   // blocks per MCU
@@ -489,12 +503,12 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArg
     const uint32_t tiles_per_row = (mw + kMcus - 1) / kMcus;
     const uint32_t ntiles = tiles_per_row * a.g.mh;
     const double scale = 255.0 / (double)a.maxval;  // Image.cpp:465
-    const bool aligned = (((uintptr_t)a.rgb | a.stride) & 15) == 0;
+    const bool aligned = (((uintptr_t)rgb_ | stride_) & 15) == 0;
     const int r8 = lane >> 3, c8 = lane & 7;  // staging: lane -> (pixel row, 16-px chunk)
     const int b8 = lane >> 3, j = lane & 7;   // DCT: lane -> (block of the round, column)
 
     const __amdgpu_buffer_rsrc_t rgb_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.rgb), 0, (int)(uint32_t)((uint64_t)a.stride * (a.g.height - 1) + 3ull * a.g.width),
+        const_cast<uint8_t*>(rgb_), 0, (int)(uint32_t)((uint64_t)stride_ * (gh_ - 1) + 3ull * gw_),
         0x00020000);
     const __amdgpu_buffer_rsrc_t coef_rs =
         __builtin_amdgcn_make_buffer_rsrc(a.coef, 0, (int)(uint32_t)((uint64_t)a.g.nblocks() * 128), 0x00020000);
@@ -507,13 +521,13 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArg
         if (lane == 0) v = atomicAdd(&lds.next, 1u);
         return __builtin_amdgcn_readfirstlane(v);
     };
-    const uint32_t lane_off = (uint32_t)r8 * (uint32_t)a.stride + (uint32_t)c8 * 48u;  // (as in fdct_kernel)
+    const uint32_t lane_off = (uint32_t)r8 * (uint32_t)stride_ + (uint32_t)c8 * 48u;  // (as in fdct_kernel)
     auto fast_load = [&](uint32_t k, uint4& v0, uint4& v1, uint4& v2) -> bool {
         const uint32_t t = tb_p + k;
         const uint32_t mrow = t / tiles_per_row, mcol0 = (t % tiles_per_row) * kMcus;
         const uint32_t y = mrow * 8 + r8, xs = mcol0 * 8 * kYh + c8 * 16;
-        const bool ok = k < n_p && aligned && y < a.g.height && xs + 16 <= a.g.width;
-        const uint32_t base = (uint32_t)((uint64_t)(mrow * 8) * a.stride + (uint64_t)mcol0 * 24 * kYh);  // (uniform)
+        const bool ok = k < n_p && aligned && y < gh_ && xs + 16 <= gw_;
+        const uint32_t base = (uint32_t)((uint64_t)(mrow * 8) * stride_ + (uint64_t)mcol0 * 24 * kYh);  // (uniform)
         const uint32_t off = ok ? base + lane_off : kOob;
         v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
         v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
@@ -576,10 +590,10 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArg
             }
         }
         if (!cfast) {  // edge replication (Image.cpp:498-531) as clamped addressing
-            const uint32_t sy = min(y, a.g.height - 1);
+            const uint32_t sy = min(y, gh_ - 1);
             for (int i = 0; i < 16; ++i) {
-                const uint32_t sx = min(xs + i, a.g.width - 1);
-                const uint8_t* p = a.rgb + (uint64_t)sy * a.stride + (uint64_t)sx * 3;
+                const uint32_t sx = min(xs + i, gw_ - 1);
+                const uint8_t* p = rgb_ + (uint64_t)sy * stride_ + (uint64_t)sx * 3;
                 px[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
             }
         }

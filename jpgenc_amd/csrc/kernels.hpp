@@ -302,10 +302,12 @@ struct FrameSet {
     uint32_t wg0[N + 1];
     uint32_t n;
 };
-// the member that owns workgroup b (uniform: scalar code)
+// the member that owns workgroup b (uniform: scalar code; a fixed trip count, so the
+// N = 1 instance reduces to member 0)
+template <int N>
 JPGE_HD inline uint32_t set_member(const uint32_t* wg0, uint32_t n, uint32_t b) {
     uint32_t f = 0;
-    for (uint32_t i = 1; i < n; ++i) f += b >= wg0[i] ? 1u : 0u;
+    for (int i = 1; i < N; ++i) f += (i < (int)n && b >= wg0[i]) ? 1u : 0u;
     return f;
 }
 template <int N = kMaxSet, typename A>
