@@ -304,6 +304,13 @@ struct FrameSet {
 };
 // the member that owns workgroup b (uniform: scalar code; a fixed trip count, so the
 // N = 1 instance reduces to member 0)
+// (K2 keeps the rolled form: with it the compiler gives the statistics kernel 62 VGPRs
+// instead of 69-70, and the kernel runs 4% faster)
+JPGE_HD inline uint32_t set_member_rolled(const uint32_t* wg0, uint32_t n, uint32_t b) {
+    uint32_t f = 0;
+    for (uint32_t i = 1; i < n; ++i) f += b >= wg0[i] ? 1u : 0u;
+    return f;
+}
 template <int N>
 JPGE_HD inline uint32_t set_member(const uint32_t* wg0, uint32_t n, uint32_t b) {
     uint32_t f = 0;

@@ -114,7 +114,7 @@ struct K2Lds {
 //     record at recbase + 1 + rank + ZRLs; one lane per block: DC and EOB.
 template <int kN>
 __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * kK2PerCu))) void stats_kernel(FrameSet<StatsArgs, kN> fs) {
-    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const uint32_t set_f = (kN == 1 ? 0u : set_member_rolled(fs.wg0, fs.n, blockIdx.x));  // (frame sets: kernels.hpp)
     const StatsArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
     __shared__ K2Lds lds;
@@ -515,7 +515,7 @@ struct K2WLds {
 
 template <int kN>
 __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_WPE))) void stats_wave_kernel(FrameSet<StatsArgs, kN> fs) {
-    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
+    const uint32_t set_f = (kN == 1 ? 0u : set_member_rolled(fs.wg0, fs.n, blockIdx.x));  // (frame sets: kernels.hpp)
     const StatsArgs& a = fs.a[set_f];
     const uint32_t bid = blockIdx.x - fs.wg0[set_f], nbk = fs.wg0[set_f + 1] - fs.wg0[set_f];
     __shared__ K2WLds L;
@@ -528,12 +528,6 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
         reinterpret_cast<uint4*>(L.key)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
 
     const uint32_t bpm = a.g.bpm, mw = a.g.mw, yh = a.g.yh, yv = a.g.yv();
-    // the arguments the sub-stream loop reads, loaded once: a set member's arguments sit
-    // at a computed kernarg offset, and the compiler otherwise reloads them in the loop
-    // (scalar loads whose lgkmcnt waits also wait for the loop's LDS traffic)
-    uint32_t rst_mcus = a.rst.mcus, rst_mcu0 = a.rst.mcu0;
-    int seed0 = a.seed.v[0], seed1 = a.seed.v[1], seed2 = a.seed.v[2];
-    asm volatile("" : "+s"(rst_mcus), "+s"(rst_mcu0), "+s"(seed0), "+s"(seed1), "+s"(seed2));
     const uint32_t yhs = (uint32_t)__builtin_ctz(yh);
     const uint32_t ybw = mw * yh;  // Y blocks per block row
     const uint32_t S = seg_tiles(a.seg) * kRecSub;
@@ -622,10 +616,10 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
             const int back = ynext ? 1 : (k == 0 ? 3 : (int)bpm);
             const bool none = !ynext && g < bpm;
             bool reset = false;
-            if (rst_mcus && (k == 0 || k >= bpm - 2)) reset = (m6 + rst_mcu0) % rst_mcus == 0;
+            if (a.rst.mcus && (k == 0 || k >= bpm - 2)) reset = (m6 + a.rst.mcu0) % a.rst.mcus == 0;
             const int dcv = __builtin_amdgcn_ds_bpermute((lane + 6) * 4, dcs);
             int pd = __builtin_amdgcn_ds_bpermute((lane + 6 - back) * 4, dcs);  // (lane - back >= -6)
-            pd = reset ? 0 : none ? (comp == 0 ? seed0 : comp == 1 ? seed1 : seed2) : pd;
+            pd = reset ? 0 : none ? (comp == 0 ? a.seed.v[0] : comp == 1 ? a.seed.v[1] : a.seed.v[2]) : pd;
             dd = (int)(int16_t)dcv - (int)(int16_t)pd;
         }
         if (sn < ns) load_dcs(sn);
