@@ -491,14 +491,6 @@ static_assert(kWCopies <= 32 && kWCopyWords % 32 == kWBankStep && kWCopyWords >=
 constexpr uint32_t kWKeyWords = (kWSyms + 1 + 3) / 4 * 4;  // keys, then one shared dummy word
 constexpr uint32_t kWMaxSubs = 1024;  // sub-streams per workgroup, at most (stats_grid)
 
-// v[lane] = x: v_writelane with the lane select in M0 (gfx950 reads one scalar
-// operand per VALU instruction besides M0), one VALU instead of a compare and a
-// select.  The statistics kernel does not use M0 otherwise (no LDS DMA, no
-// messages; checked in its ISA), so M0 is not saved around the write.
-__device__ __forceinline__ void set_lane(uint32_t& v, uint32_t x, uint32_t lane) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(lane));
-}
-
 // zig-zag position -> natural index (inverse of Coding.hpp:57-81)
 static __constant__ uint8_t kZzToNat[64] = {
     0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
@@ -632,7 +624,6 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
         uint32_t* srec = a.recs + (uint64_t)(s / kRecSub) * kTileRecords + (s % kRecSub) * kSubRecords;
         const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(srec, 0, kSubRecords * 4, 0x00020000);
         uint32_t base = 0;   // the block's first record (its DC) in the sub-stream
-        uint32_t bvec = 0;   // lane j: block j's first record
         // one block's fields (lane p: zig-zag position p)
         struct Blk {
             uint64_t M, em;     // AC non-zeros; the lanes with a record (+ lane 63: non-zero, or the EOB)
@@ -655,6 +646,12 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
             const uint32_t bits = extra_bits(c, cat);
             const uint32_t rr = c != 0 ? (b.run & 15u) : 0u;  // (the EOB lane: 0)
             b.rec = b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits;
+            // lane 0 (the DC position) carries the block's DC record, stored with the
+            // block's other records at its first record (rank 0): stored after the
+            // sub-stream, the DC records rewrote lines already written back (K2 wrote 1.24x
+            // its record bytes)
+            const uint32_t drj = __builtin_amdgcn_readlane(drec, jb);
+            b.rec = lane == 0 ? drj : b.rec;
             b.w = b.acw + (uint32_t)cat + kRunStride * rr;
             b.em = b.M | (1ull << 63);
             b.zrl = (__ballot(b.run >= 16u) & b.M) != 0;
@@ -678,6 +675,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
                     if (kz < L.key[wz]) atomicMin(&L.key[wz], kz);
                 }
             }
+            if (lane == 0) srec[base] = b.rec;  // (the DC record)
             if (__builtin_amdgcn_inverse_ballot_w64(b.em)) {
                 srec[base + b.rk] = b.rec;
                 atomicAdd(&cnt[b.w], 1u);
@@ -711,8 +709,9 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
                     // (K2W_DUMMY_ADD) or are masked off
                     baseB = base + 1u + (uint32_t)__builtin_popcountll(A.em);
                     const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
-                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
+                    // (lane 0: the DC record, at rank 0)
+                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia || lane == 0 ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib || lane == 0 ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
 #if K2W_DUMMY_ADD
                     atomicAdd(&cnt[ia ? A.w : dummy], 1u);
                     atomicAdd(&cnt[ib ? B.w : dummy], 1u);
@@ -727,24 +726,16 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
                         if (kkA < kvA) atomicMin(&L.key[kwA], kkA);
                         if (kkB < kvB) atomicMin(&L.key[kwB], kkB);
                     }
-                    set_lane(bvec, base, jb);
-                    set_lane(bvec, baseB, jb + 1);
                     base = baseB + 1u + (uint32_t)__builtin_popcountll(B.em);
                 } else {
-                    set_lane(bvec, base, jb);
                     baseB = base + emit(A, base);
-                    set_lane(bvec, baseB, jb + 1);
                     base = baseB + emit(B, baseB);
                 }
             }
-            if (jb < j1) {  // an odd last block
-                set_lane(bvec, base, jb);
-                base += emit(prep(cnA, jb), base);
-            }
+            if (jb < j1) base += emit(prep(cnA, jb), base);  // an odd last block
         }
         JPGE_ACC(2, tq);
-        if ((uint32_t)lane < nb) {  // the DC records (fields rebuilt from the words kept through the loop)
-            srec[bvec] = drec;
+        if ((uint32_t)lane < nb) {  // the DC symbols' counts and keys (their records went with their blocks)
             const uint32_t w = ((drec >> 25) ? tab_base(2) : tab_base(0)) + ((drec >> 16) & 0xFFu);
             const uint32_t rk = (acb & 0x80000000u) | ((acb & 0x7FFFFFFFu) >> 7);  // the text index
             atomicAdd(&cnt[w], 1u);
