@@ -88,3 +88,21 @@ def test_1080p_sets_match_single_frames():
     finally:
         enc.close()
         ref.close()
+
+
+def test_sets_fall_back_with_restart_then_scaled_path():
+    # restart intervals (no placement in the code kernel) launch frame by frame with the
+    # same bytes as single encodes; then sets again, on both colour paths
+    enc = _encoder(JPGE_LANES=4)
+    try:
+        frames = [J.synth_rgb8(9500 + i, 200, 136) for i in range(6)]
+        enc.set_restart(4)
+        got = enc.encode_batch(frames, quality=90)
+        assert got == [enc.encode(f, quality=90) for f in frames]
+        enc.set_restart(0)
+        scaled = [f if i % 2 else (f.astype(np.uint32) * 200 // 255).astype(np.uint8) for i, f in enumerate(frames)]
+        for maxval in (255, 200):
+            got = enc.encode_batch(scaled, quality=75, maxval=maxval)
+            assert got == [_oracle.encode(f, 75, maxval) for f in scaled]
+    finally:
+        enc.close()
