@@ -106,3 +106,29 @@ def test_sets_fall_back_with_restart_then_scaled_path():
             assert got == [_oracle.encode(f, 75, maxval) for f in scaled]
     finally:
         enc.close()
+
+
+def test_set_member_errors_stay_with_their_frame():
+    # one member of a set with too small an output buffer: that frame reports
+    # JPGE_E_NOSPACE, every other frame of the batch (its set included) is unaffected
+    import ctypes
+
+    enc = _encoder(JPGE_LANES=2)
+    try:
+        frames = [np.ascontiguousarray(J.synth_rgb8(9700 + i, 240, 160)) for i in range(7)]
+        outs = [np.zeros(J.max_jpeg_bytes(240, 160), np.uint8) for _ in frames]
+        arr = (J.Frame * len(frames))()
+        for i, (f, o) in enumerate(zip(frames, outs)):
+            arr[i].rgb, arr[i].width, arr[i].height = f.ctypes.data, 240, 160
+            arr[i].stride, arr[i].maxval = 240 * 3, 255
+            arr[i].out, arr[i].cap = o.ctypes.data, (100 if i == 2 else o.size)
+        qy, qc = J.quality_tables(90)
+        st = J.lib().jpge_encode_batch(enc._ctx, arr, len(frames), qy.ctypes.data_as(ctypes.c_void_p),
+                                       qc.ctypes.data_as(ctypes.c_void_p), 0)
+        assert st == 2 and arr[2].status == 2  # JPGE_E_NOSPACE
+        for i, f in enumerate(frames):
+            if i != 2:
+                assert arr[i].status == 0
+                assert outs[i][:arr[i].len].tobytes() == _oracle.encode(f, 90)
+    finally:
+        enc.close()
