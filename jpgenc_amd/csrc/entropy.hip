@@ -732,12 +732,39 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
         const uint32_t align = (uint32_t)(d & 3);
         if (j0 < jhi) {
             uint32_t o = align + (j0 - c) + excl;
+            if (cff == 0 && jhi - j0 == (uint32_t)kWin) {
+                // A full window without 0xFF (~88% of them): its 32 bytes go out as whole
+                // LDS words, shifted to the window's byte offset, plus the bytes of the
+                // words it shares with its neighbours (every byte has exactly one writer).
+                // 8 or 7 word stores and 4 byte stores instead of 32 byte stores, each of
+                // which conflicted 8 ways (lanes 32 bytes apart).
+                uint32_t z[kWinWords];  // little-endian: byte 4m + i of the window in bits 8i of z[m]
 #pragma unroll
-            for (int q = 0; q < kWin; ++q) {
-                if (j0 + q < jhi) {
-                    const uint8_t v = (uint8_t)(y[q >> 2] >> (24 - 8 * (q & 3)));
-                    S.ob[o++] = v;
-                    if (v == 0xFF) S.ob[o++] = 0;
+                for (int m = 0; m < kWinWords; ++m) z[m] = __builtin_bswap32(y[m]);
+                uint32_t* ob32 = reinterpret_cast<uint32_t*>(S.ob);
+                const uint32_t r = o & 3u;
+                if (r == 0) {
+#pragma unroll
+                    for (int m = 0; m < kWinWords; ++m) ob32[(o >> 2) + m] = z[m];
+                } else {
+#pragma unroll
+                    for (uint32_t q = 0; q < 3; ++q)  // the head: window bytes 0 .. 3 - r
+                        if (q < 4u - r) S.ob[o + q] = (uint8_t)(z[0] >> (8 * q));
+                    const uint32_t wb = (o + 4u - r) >> 2;  // the first whole word
+#pragma unroll
+                    for (int m = 0; m < kWinWords - 1; ++m) ob32[wb + m] = __builtin_amdgcn_alignbyte(z[m + 1], z[m], 4u - r);
+#pragma unroll
+                    for (uint32_t q = 0; q < 3; ++q)  // the tail: window bytes 32 - r .. 31
+                        if (q < r) S.ob[o + kWin - r + q] = (uint8_t)(z[kWinWords - 1] >> (8 * (4u - r + q)));
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < kWin; ++q) {
+                    if (j0 + q < jhi) {
+                        const uint8_t v = (uint8_t)(y[q >> 2] >> (24 - 8 * (q & 3)));
+                        S.ob[o++] = v;
+                        if (v == 0xFF) S.ob[o++] = 0;
+                    }
                 }
             }
         }
