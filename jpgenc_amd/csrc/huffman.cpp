@@ -333,7 +333,6 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     struct Work {
         HeapItem base[kMaxSyms], heap[2 * kCap + kHeapPad], srt_[2 * kCap + 3];
         HeapItem pk_[2][kCap + 2], lsrt_[kMaxSyms + 2];
-        uint8_t eq_[2 * kCap + 3];
         int kid_a[kMaxKids], kid_b[kMaxKids], mult[kMaxNodes], first[kMaxNodes];
     };
     static thread_local std::unique_ptr<Work> tls_work;
@@ -348,7 +347,6 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     HeapItem* const srt_ = W.srt_;
     HeapItem(*const pk_)[kCap + 2] = W.pk_;
     HeapItem* const lsrt_ = W.lsrt_;
-    uint8_t* const eq_ = W.eq_;
     constexpr HeapItem kLo = 0, kHi = ~0ull;  // sentinels: below / above every weight in use
     int nbase = 0;
     for (int i = 0; i < n; ++i) heap_push(base, nbase, item(lcnt[i], i));
@@ -373,16 +371,21 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     // harmless only when they are one pair (k odd, below pe = the paired items) and the
     // tie reaches neither k-2 nor k+1; a harmful tie's later items are harmful too, so
     // the last harmful k is the end of the last harmful tie.  (Branch-free.)
-    uint8_t* const eq = eq_ + 1;
-    auto last_tie = [srt, eq](int m, int pe) {
+    // (the flags of k-1, k and k+1 ride in registers; srt[m] = kHi ends the last tie)
+    auto last_tie = [srt](int m, int pe) {
         srt[m] = kHi;
-        for (int k = 0; k <= m; ++k) eq[k] = item_hi(srt[k]) == item_hi(srt[k - 1]);
-        eq[0] = 0;
-        eq[m] = 0;
         int e = -1;
+        uint32_t hc = item_hi(srt[0]), hn = item_hi(srt[1]);
+        bool ep = false, ec = hn == hc;  // eq[k-1], eq[k] for k = 1
+        hc = hn;
         for (int k = 1; k < m; ++k) {
-            const bool h = eq[k] & (((k & 1) == 0) | eq[k - 1] | eq[k + 1] | (k >= pe));
+            hn = item_hi(srt[k + 1]);
+            const bool en = hn == hc;  // eq[k+1]
+            const bool h = ec & (((k & 1) == 0) | ep | en | (k >= pe));
             e = h ? k : e;
+            ep = ec;
+            ec = en;
+            hc = hn;
         }
         return e;
     };
@@ -394,23 +397,22 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         if (!wrapped) {
             // levels[lv] = the leaves + levels[lv-1]'s packages, by weight, leaves first on
             // ties: a branch-free merge run from both ends at once (two independent chains)
+            // (one loop body carries both chains: a chain step waits on its loads)
             const int half = (m + 1) / 2;
-            int i = 0, j = 0;
+            int i = 0, j = 0, i2 = n - 1, j2 = np - 1;
             for (int k = 0; k < half; ++k) {
+                // from the end (an odd m's extra step reads sentinels or unused items
+                // and its slot is rewritten by the front step below)
+                const HeapItem a2 = lsrt[i2], b2 = in[j2];
+                const bool t2 = item_hi(b2) >= item_hi(a2);
+                srt[m - 1 - k] = t2 ? b2 : a2;
+                j2 -= t2;
+                i2 -= !t2;
                 const HeapItem a = lsrt[i], b = in[j];
-                const bool take = item_hi(b) < item_hi(a);
-                srt[k] = take ? b : a;
-                j += take;
-                i += !take;
-            }
-            i = n - 1;
-            j = np - 1;
-            for (int k = m - 1; k >= half; --k) {
-                const HeapItem a = lsrt[i], b = in[j];
-                const bool take = item_hi(b) >= item_hi(a);
-                srt[k] = take ? b : a;
-                j -= take;
-                i -= !take;
+                const bool t = item_hi(b) < item_hi(a);
+                srt[k] = t ? b : a;
+                j += t;
+                i += !t;
             }
             srt[-1] = kLo;
             e = last_tie(m, m - (m & 1));

@@ -22,7 +22,7 @@ int main(int argc, char** argv) {
         uint32_t cc[256] = {0};
         uint64_t kk[256];
         const int ns = 1 + (int)(rng() % 256);
-        const int mode = it % 6;
+        const int mode = it % 7;
         const uint32_t maxc = mode == 0 ? 2 : mode == 1 ? 20 : mode == 2 ? 1000 : mode == 3 ? 3000000 : 2000000000u / 256;
         std::vector<int> perm(256);
         for (int i = 0; i < 256; ++i) perm[i] = i;
@@ -31,6 +31,9 @@ int main(int argc, char** argv) {
         if (mode == 5)  // log-uniform counts, like a frame's: ties among the rare symbols and their packages
             for (int i = 0; i < ns; ++i)
                 cc[perm[i]] = (uint32_t)std::exp(std::uniform_real_distribution<double>(0.0, 20.0)(rng));
+        if (mode == 6)  // a few powers of two and small counts: whole levels of tied packages, whose order repeats
+            for (int i = 0; i < ns; ++i)
+                cc[perm[i]] = rng() % 3 ? 1u + (uint32_t)(rng() % 4) : 1u << (rng() % 16);
         for (int s = 0; s < 256; ++s) kk[s] = rng() % (mode == 4 ? 300 : 100000000);  // (ties in keys: symbol order)
         const bool a = jpge::build_table(cc, kk, t), b = jpge::build_table_std(cc, kk, u);
         if (a != b || std::memcmp(&t, &u, sizeof t) != 0) {
