@@ -453,8 +453,8 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
 // land on different copies and banks), first-occurrence keys a read and a rare
 // atomicMin; lanes without a record touch a dummy word of their own, so none of it
 // needs an exec mask.  A block with a run of 16+ zeros before a non-zero (rare)
-// takes a wave scan for its ZRL records.  The DC records of a sub-stream are stored
-// together after its blocks, lane j at block j's first record.
+// takes a wave scan for its ZRL records.  Each block's DC difference replaces its DC
+// coefficient in the stage, so lane 0 codes the DC record with the block's records.
 // Reference: DC chain Image.cpp:638-678, RLE + category Coding.hpp:148-283 and
 // Image.cpp:680-735, texts Image.cpp:888-906.
 #ifndef K2W_WAVES
@@ -464,7 +464,7 @@ __global__ __launch_bounds__(kK2Threads) __attribute__((amdgpu_waves_per_eu(2 * 
 #define K2W_COPIES 8
 #endif
 #ifndef K2W_WPE
-#define K2W_WPE 7  // waves per SIMD the register allocation targets (8: <= 64 VGPRs, 2 spilled; equal speed)
+#define K2W_WPE 8  // waves per SIMD the register allocation targets (<= 64 VGPRs: 4 workgroups per CU; 7 let the compiler take 69)
 #endif
 #ifndef K2W_DUMMY_ADD
 #define K2W_DUMMY_ADD 0  // 1: lanes without a record add into a dummy word of their own instead of being masked off
@@ -498,7 +498,7 @@ static __constant__ uint8_t kZzToNat[64] = {
     30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
 struct K2WLds {
-    alignas(16) uint32_t stage[kWWaves][8 * 32];        // each wave's 8-block chunk: int16 [block][64], natural order
+    alignas(16) uint32_t stage[kWWaves][8 * 32 + 32];   // each wave's 8-block chunk: int16 [block][64], natural order; 64 spare int16
     alignas(16) uint32_t cnt[kWCopies * kWCopyWords];    // counters [copy][word], then the dummies
     alignas(16) uint32_t key[kWKeyWords];                // first-occurrence keys (min), workgroup-relative
     uint32_t sb0[kWMaxSubs + 1];                         // the workgroup's sub-streams' first blocks, and the end
@@ -553,6 +553,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
     const uint32_t dummy = kWDummy + (uint32_t)lane;  // this lane's dummy counter word
     const uint32_t shl = (uint32_t)(64 - lane) & 63u;
     const uint64_t lanes_ac = ~1ull;  // every lane but the DC
+    const uint32_t dc_tab = lane == 0 ? 1u << 24 : 0u;  // (a record's table byte: 2t + 1 -> 2t)
     int16_t* st16 = reinterpret_cast<int16_t*>(L.stage[wv]);
     uint4* st4 = reinterpret_cast<uint4*>(L.stage[wv]);
 
@@ -644,14 +645,13 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
             b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
             const int cat = __builtin_amdgcn_frexp_expf((float)c);
             const uint32_t bits = extra_bits(c, cat);
-            const uint32_t rr = c != 0 ? (b.run & 15u) : 0u;  // (the EOB lane: 0)
-            b.rec = b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits;
-            // lane 0 (the DC position) carries the block's DC record, stored with the
-            // block's other records at its first record (rank 0): stored after the
-            // sub-stream, the DC records rewrote lines already written back (K2 wrote 1.24x
-            // its record bytes)
-            const uint32_t drj = __builtin_amdgcn_readlane(drec, jb);
-            b.rec = lane == 0 ? drj : b.rec;
+            const uint32_t rr = c != 0 && lane != 0 ? (b.run & 15u) : 0u;  // (the EOB lane, the DC lane: 0)
+            // lane 0 (the DC position, where the stage holds the block's DC difference)
+            // codes the block's DC record (its table: the AC table's number less one),
+            // stored with the block's other records at its first record (rank 0): stored
+            // after the sub-stream, the DC records rewrote lines already written back (K2
+            // wrote 1.24x its record bytes)
+            b.rec = (b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits) ^ dc_tab;
             b.w = b.acw + (uint32_t)cat + kRunStride * rr;
             b.em = b.M | (1ull << 63);
             b.zrl = (__ballot(b.run >= 16u) & b.M) != 0;
@@ -690,6 +690,11 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
             wave_order();
             if (j0 < nb) st4[lane] = cur[ch];
             cur[ch] = load_row(rsn, ch);
+            // each block's DC difference over its DC coefficient (lane j: block j)
+            // (every lane stores: the others into a slot of their own past the chunk)
+            // (8 stores on one bank per chunk: a 72-int16 block stride put them on 8 banks,
+            // but its staging index cost more than the conflicts, -0.4% in the pipeline)
+            st16[(uint32_t)lane - j0 < 8u ? ((uint32_t)lane - j0) * 64u : 512u + (uint32_t)lane] = (int16_t)dd;
             wave_order();
             if (j0 >= nb) continue;
             const uint32_t j1 = min(nb, j0 + 8u);

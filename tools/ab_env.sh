@@ -15,6 +15,6 @@ for r in $(seq $rounds); do
     echo "[$e] $(python3 -c "
 import json;d=json.loads(open('$o.json').read().strip().splitlines()[-1])
 f=lambda s:{k[:6]: round(v['avg_kernel_ms']*1e3,2) for k,v in (d.get(s) or {}).items()}
-print(d['value'], d['host_cpu']['cpus_used'], 'solo', f('stages_solo'), 'situ', f('stages'))")"
+print(d['value'], d['host_cpu']['cpus_used'], 'solo', f('stages_solo'), 'single', f('stages_solo_single_frame'), 'situ', f('stages'))")"
   done
 done
