@@ -73,6 +73,7 @@ struct K3Lds {
     uint32_t stage[kStageWords];
     uint32_t tab[4 * 256];        // (len << 16) | code
     uint32_t tcnt[kTcntSlots];    // symbol records of each sub-stream of the workgroup's tiles
+    uint32_t tcum[kTcntSlots + 2];  // their first padded stream indices, the total, then a sentinel
     alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
     uint32_t cnt8[8];
     uint32_t carry;
@@ -125,7 +126,15 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
 #endif
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
     const int ntl = (int)wt.nt * kRecSub;  // the tiles' record sub-streams (kernels.hpp)
-    if (tid < ntl) L.tcnt[tid] = a.tcount[(wt.seg * a.seg.tps + wt.t0) * kRecSub + tid];
+    if (tid < 64) {  // (wave 0: ntl <= kTcntSlots <= 64) the counts, and their padded prefix
+        static_assert(kTcntSlots <= 63, "one wave scans the sub-stream counts");
+        const uint32_t c = tid < ntl ? a.tcount[(wt.seg * a.seg.tps + wt.t0) * kRecSub + tid] : 0u;
+        if (tid < ntl) L.tcnt[tid] = c;
+        const uint32_t inc = wave_scan_incl((c + 3u) & ~3u);
+        if (tid < ntl) L.tcum[tid + 1] = inc;
+        if (tid == 0) L.tcum[0] = 0;
+        if (tid == ntl) L.tcum[ntl + 1] = ~0u;
+    }
     uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
     uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
 
@@ -164,22 +173,16 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     // valid), rounds of kRound records run across tile boundaries, and the stage is
     // flushed to R only when the next round might not fit (usually once, at the end).
     lds_barrier();  // the tile counts
-    uint32_t total = 0;  // padded records of all the workgroup's tiles
-    for (int t = 0; t < ntl; ++t) total += (L.tcnt[t] + 3u) & ~3u;
-    total = __builtin_amdgcn_readfirstlane(total);
-    uint32_t cs = 0, cpre = 0;  // this thread's tile cursor (tile, its first padded index)
-    // the thread's 4 records from stream index i (nvalid: how many are records)
+    const uint32_t total = __builtin_amdgcn_readfirstlane(L.tcum[ntl]);  // padded records of all the workgroup's tiles
+    uint32_t cs = 0;  // this thread's sub-stream cursor
+    // the thread's 4 records from stream index i (nvalid: how many are records); the
+    // cursor walks the padded prefix (the sentinel past the total stops it at ntl)
     auto rec_load = [&](uint32_t i, uint32_t& nvalid) -> uint4 {
-        while (cs < (uint32_t)ntl) {
-            const uint32_t n = (L.tcnt[cs] + 3u) & ~3u;
-            if (i < cpre + n) break;
-            cpre += n;
-            ++cs;
-        }
+        while (i >= L.tcum[cs + 1]) ++cs;
         uint32_t off = 0xFFFFFFF0u;  // (past the end: out of range, zeros)
         nvalid = 0;
         if (cs < (uint32_t)ntl) {
-            const uint32_t rel = i - cpre, c = L.tcnt[cs];
+            const uint32_t rel = i - L.tcum[cs], c = L.tcnt[cs];
             nvalid = c > rel ? min(c - rel, 4u) : 0u;
             off = (cs * slot + rel) * 4;
         }

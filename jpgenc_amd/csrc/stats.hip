@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
             b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
             const int cat = __builtin_amdgcn_frexp_expf((float)c);
             const uint32_t bits = extra_bits(c, cat);
-            const uint32_t rr = c != 0 && lane != 0 ? (b.run & 15u) : 0u;  // (the EOB lane, the DC lane: 0)
+            const uint32_t rr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? (b.run & 15u) : 0u;  // (the EOB lane, the DC lane: 0)
             // lane 0 (the DC position, where the stage holds the block's DC difference)
             // codes the block's DC record (its table: the AC table's number less one),
             // stored with the block's other records at its first record (rank 0): stored
@@ -709,9 +709,8 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
                 const Blk A = prep(cA, jb), B = prep(cB, jb + 1);
                 uint32_t baseB;
                 if (!(A.zrl || B.zrl)) {
-                    // lanes without a record store out of range (dropped) and read a shared
-                    // dummy key word; their counter adds go to a dummy word of their own
-                    // (K2W_DUMMY_ADD) or are masked off
+                    // lanes without a record store out of range (dropped); their counter adds
+                    // go to a dummy word of their own (K2W_DUMMY_ADD) or are masked off
                     baseB = base + 1u + (uint32_t)__builtin_popcountll(A.em);
                     const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
                     // (lane 0: the DC record, at rank 0)
@@ -724,12 +723,14 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(K2W_W
                     if (ia) atomicAdd(&cnt[A.w], 1u);
                     if (ib) atomicAdd(&cnt[B.w], 1u);
 #endif
-                    const uint32_t kwA = ia ? A.w : kWSyms, kwB = ib ? B.w : kWSyms;
-                    const uint32_t kvA = L.key[kwA], kvB = L.key[kwB];
-                    const uint32_t kkA = ia ? A.acbj + k2p : ~0u, kkB = ib ? B.acbj + k2p : ~0u;
-                    if (__ballot(kkA < kvA || kkB < kvB)) {  // (rare: a first occurrence in this workgroup so far)
-                        if (kkA < kvA) atomicMin(&L.key[kwA], kkA);
-                        if (kkB < kvB) atomicMin(&L.key[kwB], kkB);
+                    // (every lane reads its word: a lane without a record has c = 0, so its
+                    // word is its table's first, and lane 0's is in range too)
+                    const uint32_t kvA = L.key[A.w], kvB = L.key[B.w];
+                    const uint32_t kkA = A.acbj + k2p, kkB = B.acbj + k2p;
+                    const bool fa = ia && kkA < kvA, fb = ib && kkB < kvB;
+                    if (__ballot(fa || fb)) {  // (rare: a first occurrence in this workgroup so far)
+                        if (fa) atomicMin(&L.key[A.w], kkA);
+                        if (fb) atomicMin(&L.key[B.w], kkB);
                     }
                     base = baseB + 1u + (uint32_t)__builtin_popcountll(B.em);
                 } else {
