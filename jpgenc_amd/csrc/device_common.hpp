@@ -220,7 +220,10 @@ __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total
         if (kLdsSync) lds_barrier();
         else __syncthreads();
     }
-    if (lane == 63) ws[wv] = incl;
+    // (wv is the wave's number, uniform: in an SGPR the wave's base is summed on the
+    // scalar unit; as a VGPR it took a move and a select per wave sum, every call)
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    if (lane == 63) ws[wvu] = incl;
     if (kLdsSync) lds_barrier();
     else __syncthreads();
     T base = 0;
@@ -228,7 +231,7 @@ __device__ __forceinline__ T block_scan(T v, W* wsum, int lane, int wv, T& total
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
         const T s = ws[w];
-        if (w < wv) base += s;
+        if (w < wvu) base += s;
         total += s;
     }
     return base + incl - v;
