@@ -71,7 +71,7 @@ struct K3Lds {
     // the tile's big-endian bit stream (offset 0 of the kernel's only __shared__ object,
     // so 16-byte aligned; an alignas(16) here made the compiler spill 8 VGPRs)
     uint32_t stage[kStageWords];
-    uint32_t tab[4 * 256];        // (len << 16) | code
+    uint32_t tab[4 * 256];        // lds_tab_entry: code | (len + extra bits) << 16 | extra bits << 24
     uint32_t tcnt[kTcntSlots];    // symbol records of each sub-stream of the workgroup's tiles
     uint32_t tcum[kTcntSlots + 2];  // their first padded stream indices, the total, then a sentinel
     alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
@@ -91,14 +91,23 @@ __device__ __forceinline__ uint32_t byte_range(int lo, int hi) {
     return ge & lt & 0x80808080u;
 }
 
-// One symbol record (K2, kernels.hpp) as code bits: the table's code, then the
-// extra bits (the category's count of them); returns the bit count (<= 16 + 15).
+// The code kernel's LDS table entry for table t, symbol s: the code (bits 0-15), the
+// code length plus the symbol's extra-bit count (bits 16-23), the extra-bit count
+// (bits 24-31: AC, the symbol's size; DC, its category).  Host entries are
+// (len << 16) | code.
+__device__ __forceinline__ uint32_t lds_tab_entry(uint32_t host, uint32_t i) {
+    const uint32_t t = i >> 8, sym = i & 0xFF;
+    const uint32_t nb = (t & 1) ? (sym & 15) : (sym & 31);
+    return (nb << 24) | (((host >> 16) + nb) << 16) | (host & 0xFFFF);
+}
+// One symbol record (K2, kernels.hpp: table << 24 | symbol << 16 | extra bits) as code
+// bits: the table's code, then the extra bits; returns the bit count (<= 16 + 16).
+// (The record's top half is the entry's index; the extra-bit count rides in the entry,
+// so a record costs a read, two extracts, a shift and an OR.)
 __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, uint32_t& bits) {
-    const uint32_t sym = (r >> 16) & 0xFF, t = r >> 24;
-    const uint32_t nb = (t & 1) ? (sym & 15) : sym;  // AC: the symbol's size; DC: its category
-    const uint32_t ent = tab[(t << 8) | sym];
-    bits = ((ent & 0xFFFF) << nb) | (r & 0xFFFF);
-    return (ent >> 16) + nb;
+    const uint32_t ent = tab[r >> 16];
+    bits = ((ent & 0xFFFF) << (ent >> 24)) | (r & 0xFFFF);
+    return (ent >> 16) & 0xFF;
 }
 
 // every workgroup's WgPlace from the records (the placement scan), kK3Threads threads
@@ -117,7 +126,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         export_hist<kK3Threads>(a.exp_hist, a.exp_cnt, a.exp_key, a.exp_seq, a.exp_seqv, tid);
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
-    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = a.tables[i];
+    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = lds_tab_entry(a.tables[i], (uint32_t)i);
 #if K3_ZERO128
     static_assert(kStageWords % 4 == 0, "the stage zeroes in 16-byte stores");
     for (int i = tid; i < kStageWords / 4; i += kK3Threads) reinterpret_cast<uint4*>(L.stage)[i] = make_uint4(0, 0, 0, 0);
