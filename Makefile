@@ -17,15 +17,16 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -W
 
 HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp coding.cpp group.cpp
 HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))
-DEV_SRCS  := fdct.hip stats.hip entropy.hip planes.hip hufftab.hip
+DEV_SRCS  := fdct.hip stats.hip entropy.hip planes.hip
 DEV_OBJS  := $(addprefix $(BUILD)/,$(DEV_SRCS:.hip=.o))
 DIAG_OBJS := $(addprefix $(BUILD)/diag/,$(DEV_SRCS:.hip=.o))
 HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h
 FACADE_TEST := tests/cpp/bin/test_facade
 HUFF_TEST   := tests/cpp/bin/test_huffman_fast
 QUANT_TEST  := tests/cpp/bin/test_quant_fast
+EXIT_TEST   := tests/cpp/bin/test_exit_close
 
-all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) $(HUFF_TEST) $(QUANT_TEST) oracle
+all: $(LIBDIR)/libjpge.so $(BINDIR)/jpgenc $(FACADE_TEST) $(HUFF_TEST) $(QUANT_TEST) $(EXIT_TEST) oracle
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HEADERS)
 	@mkdir -p $(BUILD)
@@ -67,6 +68,12 @@ clean:
 # the facade under the reference's unit tests (tests/cpp/test_facade.cpp; run by
 # tests/test_facade.py): compiled exactly as reference code would be, global names
 $(FACADE_TEST): tests/cpp/test_facade.cpp $(LIBDIR)/libjpge.so $(SRC)/jpge_image.hpp include/jpge.h
+	@mkdir -p tests/cpp/bin
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -ljpge -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' \
+	  -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+
+# a caller's exit-time close after the library's own exit handler (tests/test_gpu_teardown.py)
+$(EXIT_TEST): tests/cpp/test_exit_close.cpp $(LIBDIR)/libjpge.so include/jpge.h
 	@mkdir -p tests/cpp/bin
 	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -ljpge -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' \
 	  -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib

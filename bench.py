@@ -17,8 +17,9 @@ Huffman-table build, entropy code + pack kernels, finished .jpg bytes in HBM):
              collective; the gloo group only carries barriers and the max time).
   batch1080  (config 4): one batch of 256 distinct 1920x1080 Q90 frames (seeds
              1000+i) per step, dealt over the ranks (frame i -> rank i mod N:
-             strong scaling); the .jpg segments are gathered to rank 0 over RCCL
-             (grouped send/recv) inside the step.
+             strong scaling); each rank's .jpg bytes go to rank 0 in one transfer
+             (RCCL send/recv; HIP IPC when ranks share a GPU), overlapped with the
+             next step's encode.
   16k-striped (config 5): one 16384^2 frame per step, row-striped over the ranks.
   ppm-files  (SURVEY 8(f) rank 1): PPM files -> .jpg files (PCIe-inclusive).
 
@@ -26,7 +27,8 @@ The 4k-frames line carries: `roofline` = the dominant kernel alone on the GPU (i
 exclusive time: a 1-lane encoder after the timed region, HIP events bound to the
 kernel's own dispatch; checked against the step: launches x duration <= ms_per_step),
 `roofline_dct_stage` = K1 alone (the BASELINE figure, with its HBM-read-only
-fraction), `roofline_pipeline`, per-kernel rooflines in situ (`stages`, overlapping
+fraction), `latency` (one frame per jpge_encode_rgb8 call, device and pinned-host
+buffers: the reference's one-image-per-call path), `roofline_pipeline`, per-kernel rooflines in situ (`stages`, overlapping
 lanes: diagnostic) and alone (`stages_solo`; algorithmic bytes per launch, DESIGN.md
 §4), `devices` (ranks, distinct GPUs, ranks per GPU), `verified` (every output of
 the last timed step byte-compared with the host-path encode of its frame, and a
@@ -81,6 +83,8 @@ def parse(argv=None):
     ap.add_argument("--solo-batches", type=int, default=2,
                     help="batches through a 1-lane encoder after the timed region (kernel times alone; 0 = skip)")
     ap.add_argument("--solo-warmup", type=int, default=8, help="untimed batches before the solo pass's timed ones")
+    ap.add_argument("--latency-calls", type=int, default=128,
+                    help="4k-frames: single-frame jpge_encode_rgb8 calls timed for the latency key (0 = skip)")
     ap.add_argument("--lanes", type=int, default=0, help="encoder lanes (0 = library default)")
     ap.add_argument("--workload", choices=["4k-frames", "batch1080", "16k-striped", "ppm-files", "dist-check"],
                     default="4k-frames",
@@ -185,6 +189,28 @@ def sum_over_ranks(pg, v: float) -> float:
     t = torch.tensor([v], dtype=torch.float64)
     pg.all_reduce(t, op=pg.ReduceOp.SUM)
     return float(t.item())
+
+
+def all_gather_floats(pg, v: float, world: int) -> list[float]:
+    """Every rank's value, in rank order (on rank 0; a list of one without a group)."""
+    if pg is None:
+        return [v]
+    import torch
+
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    pg.all_gather(out, torch.tensor([v], dtype=torch.float64))
+    return [float(t.item()) for t in out]
+
+
+def process_cpu_s() -> float:
+    """CPU seconds used by this process (every thread, user + system)."""
+    t = os.times()
+    return t.user + t.system
+
+
+GATHER_NAMES = {"p2p": "RCCL isend/irecv over xGMI",
+                "ipc": "HIP IPC into rank 0's buffers: the ranks share one GPU, which RCCL refuses",
+                "gloo (host-staged)": "gloo through host memory"}
 
 
 def visible_devices() -> int:
@@ -554,47 +580,79 @@ def run_batch1080(args, rank, local, world, pg):
     cap = out_capacity(J, W, H)
     host = {i: J.synth_rgb8(batch_seed(i), W, H) for i in share}
     ins = {i: torch.from_numpy(host[i].reshape(-1)).to(dev) for i in share}
-    outbuf = torch.empty(len(share) * cap, dtype=torch.uint8, device=dev)
     frames = [(ins[i].data_ptr(), W, H, W * 3) for i in share]
-    outd = [(outbuf.data_ptr() + k * cap, cap) for k in range(len(share))]
     enc = J.Encoder(local, lanes=args.lanes)
-    gather = None
+    gather, transport = None, None
+    nsets = 1
     if world > 1:
         import torch.distributed as dist
 
         from jpgenc_amd.gather import BatchGather
 
-        rccl = gather_group(world)
-        xdev = dev if dist.get_backend(rccl) == "nccl" else "cpu"  # (gloo: ranks sharing one GPU)
-        gather = BatchGather(rccl, dist.new_group(backend="gloo"), rank, world, B, len(share) * cap, xdev)
-        segs = [outbuf[k * cap:(k + 1) * cap] for k in range(len(share))]
+        meta = dist.new_group(backend="gloo")
+        if args.devices["shared"]:  # ranks on one GPU: RCCL refuses them; rank 0's buffers over HIP IPC
+            gather = BatchGather(None, meta, rank, world, B, len(share) * cap, dev, transport="ipc")
+            if gather.transport != "ipc":  # (no IPC: stage through the host over gloo)
+                gather = BatchGather(dist.new_group(backend="gloo"), meta, rank, world, B, len(share) * cap, "cpu")
+        else:
+            gather = BatchGather(gather_group(world), meta, rank, world, B, len(share) * cap, dev)
+        transport = gather.transport if gather.cuda else "gloo (host-staged)"
+        nsets = 2  # output slots alternate, so the next encode never waits for this step's pack
+    outbuf = torch.empty(nsets * len(share) * cap, dtype=torch.uint8, device=dev)
+    base = len(share) * cap
+    outd = [[(outbuf.data_ptr() + s * base + k * cap, cap) for k in range(len(share))] for s in range(nsets)]
+    segs = [[outbuf[s * base + k * cap:s * base + (k + 1) * cap] for k in range(len(share))] for s in range(nsets)]
+    phase = collections.Counter()
 
     def step():
         # encode this rank's share; then pack its .jpg bytes and post them to rank 0 as
-        # one message, which moves while the next step encodes (jpgenc_amd/gather.py)
-        lens = enc.encode_batch_dev(frames, outd, quality=args.quality)
+        # one transfer, which moves while the next step encodes (jpgenc_amd/gather.py)
+        t0 = time.perf_counter()
+        s = gather.acquire() if gather is not None else 0
+        t1 = time.perf_counter()
+        lens = enc.encode_batch_dev(frames, outd[s], quality=args.quality)
+        t2 = time.perf_counter()
         if gather is not None:
-            gather.post(segs if xdev == dev else [outbuf[k * cap:k * cap + n].cpu() for k, n in enumerate(lens)], lens)
-        return lens
+            if gather.cuda:
+                gather.post(segs[s], lens)
+            else:
+                gather.post([segs[s][k][:n].cpu() for k, n in enumerate(lens)], lens)
+        t3 = time.perf_counter()
+        phase["acquire"] += t1 - t0
+        phase["encode"] += t2 - t1
+        phase["gather_post"] += t3 - t2
+        return lens, s
 
     for _ in range(args.warmup):
         step()
+    if gather is not None:
+        gather.wait()
     torch.cuda.synchronize()
     barrier(pg)
+    phase.clear()
+    if gather is not None:
+        gather.lens_wait_s = 0.0
     cg0 = cgroup_cpu_stat()
+    pc0 = process_cpu_s()
     th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens = step()
+        lens, s_last = step()
+    t1 = time.perf_counter()
     if gather is not None:
         gather.wait()
     torch.cuda.synchronize()
     barrier(pg)
     dt = time.perf_counter() - t0
+    phase["final_wait"] = dt - (t1 - t0)
     cg1 = cgroup_cpu_stat()
+    pcpu = (process_cpu_s() - pc0) / dt
     thread_report(th0, dt)
     dt_max = max_over_ranks(pg, dt)
     nbytes = sum_over_ranks(pg, float(sum(lens)))
+    rank_cpus = all_gather_floats(pg, pcpu, world)
+    if gather is not None and rank == 0:
+        phase["lengths_wait"] = gather.lens_wait_s
     # verification: every frame of the last step, as rank 0 holds it, equals the
     # host-path encode of that frame (rank 0's own frames are in its output slots)
     bad = 0
@@ -604,7 +662,7 @@ def run_batch1080(args, rank, local, world, pg):
                 ref = enc.encode(host[i] if i in host else J.synth_rgb8(batch_seed(i), W, H), quality=args.quality)
                 if i in host:
                     k = share.index(i)
-                    got = outbuf[k * cap:k * cap + lens[k]]
+                    got = segs[s_last][k][:lens[k]]
                 else:
                     got = gather.frame(i).to(dev)
                 if not torch.equal(got, torch.frombuffer(bytearray(ref), dtype=torch.uint8).to(dev)):
@@ -618,8 +676,9 @@ def run_batch1080(args, rank, local, world, pg):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 photo-like frames, seeds 1000+i, HBM-resident)",
             "config": {"workload": f"config 4: {B} x {W}x{H} 4:2:0 Q{args.quality} per step, frame i on rank i mod "
-                                   f"{world}" + (", each rank's .jpg bytes packed and sent to rank 0 as one RCCL "
-                                                 "message, overlapped with the next step's encode" if world > 1 else ""),
+                                   f"{world}" + (f", each rank's .jpg bytes packed and moved to rank 0 in one transfer "
+                                                 f"({GATHER_NAMES.get(transport, transport)}), overlapped with the "
+                                                 f"next step's encode" if world > 1 else ""),
                        "batch": B, "width": W, "height": H, "quality": args.quality,
                        "avg_jpeg_bytes": int(nbytes / B), "parallelism": f"frames dealt over {world} GPU(s)"},
             "verified": None if args.no_verify else {
@@ -627,6 +686,8 @@ def run_batch1080(args, rank, local, world, pg):
                 "method": "every frame of the last step, as gathered on rank 0, byte-compared with the host-path "
                           "encode of the same frame"},
             "host_cpu": host_cpu_use(cg0, cg1, dt),
+            "rank_cpus": [round(c, 2) for c in rank_cpus],
+            "rank0_phases_ms_per_step": {k: round(v / args.steps * 1e3, 3) for k, v in phase.items()},
             "devices": args.devices,
         }
         print(json.dumps(line), flush=True)
@@ -776,14 +837,50 @@ def run_frames(args, rank, local, world, pg):
         tm_solo, solo_win = solo_pass(set_size)
         tm_solo1, solo1_win = solo_pass(1) if set_size > 1 else (tm_solo, solo_win)
 
+    # Single-image latency on the drop-in path (main.cpp:29 -> Image::writeJPEG, one image
+    # per call): jpge_encode_rgb8 on a 1-lane context, one frame per call, wall time per
+    # call; device-in/device-out and pinned host-in/host-out (PCIe copies inside the call)
+    latency = None
+    if args.latency_calls > 0:
+        lat = J.Encoder(local, lanes=1)
+        lat.set_subsampling(args.subsampling)
+        hin = [torch.from_numpy(host[d].reshape(-1)).pin_memory() for d in range(min(D, 8))]
+        hout = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+
+        def series(call):
+            for i in range(8):
+                call(i)
+            ts = []
+            for i in range(args.latency_calls):
+                t = time.perf_counter()
+                call(i)
+                ts.append((time.perf_counter() - t) * 1e3)
+            ts.sort()
+            return {"median_ms": round(ts[len(ts) // 2], 4), "p99_ms": round(ts[min(len(ts) - 1, int(0.99 * len(ts)))], 4),
+                    "min_ms": round(ts[0], 4), "calls": len(ts)}
+
+        latency = {
+            "device_in_device_out": series(lambda i: lat.encode_ptr(frames[i % D][0], W, H, pitch, outd[0][0], cap,
+                                                                    quality=args.quality)),
+            "host_in_host_out": series(lambda i: lat.encode_ptr(hin[i % len(hin)].data_ptr(), W, H, pitch,
+                                                                hout.data_ptr(), cap, quality=args.quality, flags=0)),
+            "what": f"one {W}x{H} frame per jpge_encode_rgb8 call on a 1-lane context (the reference's one image per "
+                    f"writeJPEG call), wall time per call; host buffers pinned",
+        }
+        lat.close()
+        del hin, hout
+
     # per-kernel rooflines (HBM-bound integer/fp64 work; algorithmic bytes per launch)
     npx = W * H
     avg_jpeg = total_bytes / (args.steps * F)
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H) if args.subsampling == 420 else {}
     yh, yv = J.SUBSAMPLING[args.subsampling]
     cb = 2.0 * 64 * (yh * yv + 2) / (64 * yh * yv)  # int16 coefficient bytes per pixel (4:2:0: 3)
-    # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3
-    rec_bytes = 4.0 * tm["symbols"] / max(1, tm["frames"])
+    # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3;
+    # the count per frame from every distinct input's histograms (whether or not a pass
+    # sampled it), averaged over the step's frames (frame i = input i mod D)
+    syms = [int(enc.symbol_stats(host[d], quality=args.quality)[0].sum()) for d in range(D)]
+    rec_bytes = 4.0 * sum(syms[i % D] for i in range(F)) / F
     # per-kernel algorithmic bytes per launch; the entropy stage is two
     # kernels: code (records -> the unstuffed bit stream) and pack (-> stuffed .jpg)
     alg = {
@@ -803,11 +900,19 @@ def run_frames(args, rank, local, world, pg):
         nl = max(1, tm.get("launches") or tm["frames"])
         fpl = tm["frames"] / nl if tm["frames"] else 1.0
         out = {}
+        timed = bool(tm.get("launches") or tm["frames"])
         for name, (b, what) in list(alg.items()) + list(stage_alg.items()):
             ms = tm[tm_key[name]] / nl
             bl = b * fpl
-            ach = bl / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # (0: --no-kernel-events)
             tr = traffic.get(pmc_key.get(name, name))
+            if not timed or ms <= 0:  # (no launch of this pass was timed: no figure, not a zero)
+                out[name] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                             "traffic": int(tr * fpl) if tr else tr, "alg_bytes_per_launch": int(bl),
+                             "alg_bytes": what, "avg_kernel_ms": None, "timed_launches": 0,
+                             "reason": "no launch of this kernel was timed in this pass (kernel events off or "
+                                       "no sampled frame)"}
+                continue
+            ach = bl / (ms * 1e-3) / 1e9
             out[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(tr * fpl) if tr else tr,
                          "alg_bytes_per_launch": int(bl), "alg_bytes": what, "avg_kernel_ms": round(ms, 5),
@@ -831,7 +936,7 @@ def run_frames(args, rank, local, world, pg):
     # kernels overlap, so an in-situ duration is wall time shared with the other lanes.
     roofline = None
     if stages_solo:
-        dominant = max(alg, key=lambda k: stages_solo[k]["avg_kernel_ms"])
+        dominant = max(alg, key=lambda k: stages_solo[k]["avg_kernel_ms"] or 0.0)
         roofline = dict(kernel=dominant, timing="solo (1-lane encoder after the timed region; HIP events bound "
                                                 "to the kernel's dispatch, hipExtLaunchKernel)", **stages_solo[dominant])
         # exclusive time of one launch x launches per step cannot exceed the step
@@ -842,10 +947,10 @@ def run_frames(args, rank, local, world, pg):
         if spent > ms_step:
             raise SystemExit(f"bench: roofline check failed: {lps:.1f} launches x {roofline['avg_kernel_ms']} ms "
                              f"= {spent:.3f} ms > {ms_step:.3f} ms per step")
-    elif stages["fdct_kernel"]["avg_kernel_ms"] > 0:
+    elif stages["fdct_kernel"]["avg_kernel_ms"]:
         # no solo pass (--solo-batches 0): the in-situ figure, labelled as such (lanes
         # overlap, so it is shared wall time and carries no per-step check)
-        dominant = max(alg, key=lambda k: stages[k]["avg_kernel_ms"])
+        dominant = max(alg, key=lambda k: stages[k]["avg_kernel_ms"] or 0.0)
         roofline = dict(kernel=dominant, timing="in situ (4 lanes overlap: shared wall time, not exclusive; "
                                                 "run with --solo-batches > 0 for the exclusive figure)",
                         **stages[dominant])
@@ -899,6 +1004,7 @@ def run_frames(args, rank, local, world, pg):
             "lanes": enc.lanes(),
             "verified": verified,
             "d2h": d2h,
+            "latency": latency,
             # CLOCK_MONOTONIC windows (rocprofv3 timestamps use the same clock): tools/rocprof_window.py
             "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win, "solo_single": solo1_win},
             # host CPU use over the timed region; quota throttling stalls the pipeline

@@ -80,6 +80,11 @@ int jpge_open(int device, jpge_ctx** ctx);
 /* jpge_open with an explicit lane count (0 = JPGE_LANES or the default 4; at most 8;
  * 1 = a single pipeline, e.g. to time kernels without other frames beside them). */
 int jpge_open_ex(int device, int lanes, jpge_ctx** ctx);
+/* Contexts and groups still open when the process exits are released by the library
+ * itself (an std::atexit handler registered at the first jpge_open): their threads,
+ * streams and memory are freed, but the handle stays valid, so a jpge_close or
+ * jpge_group_close the caller makes later (e.g. from its own exit handler) is a no-op,
+ * and any other call on it returns JPGE_E_ARG. */
 int jpge_close(jpge_ctx* ctx);
 /* Kernel timing with HIP events on the encoder's stream: every = 0 off, N >= 1
  * times the kernels of every N-th frame (1 = all; events cost GPU time). */
@@ -165,15 +170,6 @@ int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], ui
 /* Same for an arbitrary int symbol text (the reference signature, for tests and
  * tools): writes n distinct symbols as (symbol, length, code) in DHT order. */
 int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t* codes, int* nsym);
-
-/* The same table build on the GPU (hufftab.hip; the encoder's pipeline runs it on
- * K2's histograms): nsets sets of the four tables of a frame, host arrays
- * counts/first [nsets][4][256] in, per table (len << 16) | code [nsets][4][256],
- * the DHT piece (class/id, bits[16], huffval) [nsets][4][273] and the symbol
- * count [nsets][4] out.  Replaces generateHuffmanCode (Huffman.hpp:53) on the
- * device; equal to jpge_huffman_table table by table.  device: the GPU to use. */
-int jpge_huffman_tables_device(int device, const uint32_t* counts, const uint64_t* first, int nsets, uint32_t* tab,
-                               uint8_t* dht, uint32_t* nsym);
 
 /* ---- Decode-side verification utilities (host) ---- */
 

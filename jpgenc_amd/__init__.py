@@ -38,7 +38,7 @@ EXPORTS = (
     "jpge_strerror", "jpge_version", "jpge_device_count", "jpge_open", "jpge_open_ex", "jpge_close", "jpge_set_timing",
     "jpge_get_timing", "jpge_reset_timing", "jpge_get_lanes", "jpge_set_restart_interval", "jpge_set_subsampling",
     "jpge_max_jpeg_bytes", "jpge_quality_tables", "jpge_encode_rgb8", "jpge_encode_batch",
-    "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_tables_device", "jpge_huffman_text", "jpge_parse_ppm",
+    "jpge_fdct_quant", "jpge_symbol_stats", "jpge_huffman_table", "jpge_huffman_text", "jpge_parse_ppm",
     "jpge_ppm_info", "jpge_encode_file", "jpge_encode_files", "jpge_synth_rgb8", "jpge_arai_constants",
     "jpge_stripe_transform", "jpge_stripe_stats", "jpge_stripe_code", "jpge_stripe_place", "jpge_stripe_pack",
     "jpge_huffman_decode", "jpge_idct8x8", "jpge_decode_coeffs",
@@ -142,7 +142,6 @@ def lib() -> ctypes.CDLL:
         L.jpge_stripe_pack.argtypes = [vp, ctypes.POINTER(StripeSummary), i32, i32, vp, sz, ctypes.POINTER(sz),
                                        ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.jpge_huffman_table.argtypes = [vp, vp, vp, vp, ctypes.POINTER(i32), vp, vp]
-        L.jpge_huffman_tables_device.argtypes = [i32, vp, vp, i32, vp, vp, vp]
         L.jpge_huffman_text.argtypes = [vp, sz, vp, vp, vp, ctypes.POINTER(i32)]
         L.jpge_parse_ppm.argtypes = [vp, sz, vp, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
                                      ctypes.POINTER(i32)]
@@ -299,21 +298,6 @@ def huffman_table(counts, first):
     _check(lib().jpge_huffman_table(_p(c), _p(f), _p(bits), _p(hv), ctypes.byref(n), _p(code), _p(ln)),
            "huffman_table")
     return bits, hv[:n.value].tolist(), code, ln
-
-
-def huffman_tables_device(counts, first, device: int = 0):
-    """The table build on the GPU (hufftab.hip) for sets of a frame's four tables:
-    counts/first [nsets, 4, 256] -> (tab [nsets, 4, 256] = len << 16 | code,
-    dht [nsets, 4, 273] = class/id, bits[16], huffval, nsym [nsets, 4])."""
-    c = np.ascontiguousarray(counts, dtype=np.uint32).reshape(-1, 4, 256)
-    f = np.ascontiguousarray(first, dtype=np.uint64).reshape(-1, 4, 256)
-    n = c.shape[0]
-    tab = np.zeros((n, 4, 256), np.uint32)
-    dht = np.zeros((n, 4, 273), np.uint8)
-    ns = np.zeros((n, 4), np.uint32)
-    _check(lib().jpge_huffman_tables_device(int(device), _p(c), _p(f), n, _p(tab), _p(dht), _p(ns)),
-           "huffman_tables_device")
-    return tab, dht, ns
 
 
 # ---- Coding.hpp primitives (host, C ABI) ----
@@ -490,6 +474,19 @@ class Encoder:
         _check(lib().jpge_encode_rgb8(self._ctx, _p(rgb), w, h, w * 3, int(maxval), _p(qy), _p(qc), _p(out),
                                       out.size, ctypes.byref(n), 0), "encode")
         return out[:n.value].tobytes()
+
+    def encode_ptr(self, rgb_ptr: int, w: int, h: int, stride: int, out_ptr: int, cap: int, quality: int = 50,
+                   maxval: int = 255, flags: int = JPGE_DEVICE_INPUT | JPGE_DEVICE_OUTPUT) -> int:
+        """One frame through jpge_encode_rgb8 on raw pointers (device or host per `flags`;
+        host pointers may be pinned memory); returns the .jpg length."""
+        q = self._qcache.get(quality)
+        if q is None:
+            qy, qc = self._tables(quality, None, None)
+            q = self._qcache[quality] = (qy, qc, _p(qy), _p(qc))
+        n = ctypes.c_size_t()
+        _check(lib().jpge_encode_rgb8(self._ctx, rgb_ptr, w, h, stride, int(maxval), q[2], q[3], out_ptr, cap,
+                                      ctypes.byref(n), int(flags)), "encode_rgb8")
+        return n.value
 
     def encode_batch_dev(self, frames: list[tuple[int, int, int, int]], outs: list[tuple[int, int]],
                          quality: int = 50, maxval: int = 255,

@@ -44,12 +44,15 @@ struct LiveSet {
     std::mutex mu;
     std::vector<jpge_ctx*> ctx;
     std::vector<jpge_group*> grp;
+    // handles the exit handler released: their resources are gone, the handle stays valid
+    // so that a caller's own later jpge_close / jpge_group_close is a no-op
+    std::vector<const void*> dead;
 };
 LiveSet& live() {
     static LiveSet* s = new LiveSet();  // never destroyed: it must outlive every exit handler
     return *s;
 }
-// (live.hpp) closes every group, then every context, still open at exit
+// (live.hpp) releases every group, then every context, still open at exit
 void close_live_at_exit() {
     for (;;) {
         jpge_group* g = nullptr;
@@ -58,7 +61,7 @@ void close_live_at_exit() {
             if (!live().grp.empty()) g = live().grp.back();
         }
         if (!g) break;
-        jpge_group_close(g);  // (removes itself and closes its member contexts)
+        live_release(g);  // (group.cpp: its RCCL communicators and member contexts too)
     }
     for (;;) {
         jpge_ctx* c = nullptr;
@@ -67,7 +70,7 @@ void close_live_at_exit() {
             if (!live().ctx.empty()) c = live().ctx.back();
         }
         if (!c) break;
-        jpge_close(c);
+        live_release(c);
     }
 }
 void forget_in_child() {  // a forked child: the parent's lane threads do not exist here
@@ -103,6 +106,23 @@ void live_add(jpge_group* g) {
 void live_remove(jpge_group* g) {
     std::lock_guard<std::mutex> l(live().mu);
     erase_one(live().grp, g);
+}
+bool live_is_released(const void* h) {
+    std::lock_guard<std::mutex> l(live().mu);
+    return std::find(live().dead.begin(), live().dead.end(), h) != live().dead.end();
+}
+void live_mark_released(const void* h) {
+    std::lock_guard<std::mutex> l(live().mu);
+    live().dead.push_back(h);
+}
+void live_release(jpge_ctx* c) {
+    live_remove(c);
+    if (c->enc) {  // wait for a call still running on another thread, then tear down
+        { std::lock_guard<std::recursive_mutex> wait(c->enc->call_mutex()); }
+        c->enc.reset();
+    }
+    c->ingest.reset();
+    live_mark_released(c);
 }
 void live_handler_after_load() {
     static std::once_flag once;
@@ -153,19 +173,20 @@ int jpge_open_ex(int device, int lanes, jpge_ctx** ctx) {
 }
 
 int jpge_close(jpge_ctx* ctx) {
-    if (ctx) jpge::live_remove(ctx);
+    if (!ctx || jpge::live_is_released(ctx)) return JPGE_OK;  // (released at exit: live.hpp)
+    jpge::live_remove(ctx);
     delete ctx;
     return JPGE_OK;
 }
 
 int jpge_set_timing(jpge_ctx* ctx, int every) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     ctx->enc->set_timing(every);
     return JPGE_OK;
 }
 
 int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
-    if (!ctx || !t) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !t) return JPGE_E_ARG;
     const auto& k = ctx->enc->times();
     t->fdct = k.fdct;
     t->dc_stats = k.dc_stats;
@@ -183,24 +204,24 @@ int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
 }
 
 int jpge_reset_timing(jpge_ctx* ctx) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     ctx->enc->reset_timing();
     return JPGE_OK;
 }
 
 int jpge_get_lanes(jpge_ctx* ctx, int* lanes) {
-    if (!ctx || !lanes) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !lanes) return JPGE_E_ARG;
     *lanes = ctx->enc->lanes();
     return JPGE_OK;
 }
 
 int jpge_set_restart_interval(jpge_ctx* ctx, uint32_t mcus) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     return ctx->enc->set_restart(mcus) ? JPGE_E_ARG : JPGE_OK;
 }
 
 int jpge_set_subsampling(jpge_ctx* ctx, int mode) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     return ctx->enc->set_subsampling(mode) ? JPGE_E_ARG : JPGE_OK;
 }
 
@@ -215,7 +236,7 @@ int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]) {
 int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
                      const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len,
                      uint32_t flags) {
-    if (!ctx || !rgb || !qy || !qc || !out || !len) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !out || !len) return JPGE_E_ARG;
     jpge::FrameDesc f = frame(rgb, w, h, stride, maxval);
     f.out = out;
     f.cap = cap;
@@ -226,7 +247,7 @@ int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, 
 
 int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
                       uint32_t flags) {
-    if (!ctx || (!frames && n) || n < 0 || !qy || !qc) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || (!frames && n) || n < 0 || !qy || !qc) return JPGE_E_ARG;
     std::vector<jpge::FrameDesc> fd(n);
     for (int i = 0; i < n; ++i) {
         fd[i] = frame(frames[i].rgb, frames[i].width, frames[i].height, frames[i].stride, frames[i].maxval);
@@ -244,80 +265,15 @@ int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy
 int jpge_fdct_quant(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
                     const uint8_t qy[64], const uint8_t qc[64], int16_t* cy, int16_t* ccb, int16_t* ccr,
                     uint32_t flags) {
-    if (!ctx || !rgb || !qy || !qc || !cy || !ccb || !ccr) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !cy || !ccb || !ccr) return JPGE_E_ARG;
     return ctx->enc->fdct_quant(frame(rgb, w, h, stride, maxval), qy, qc, flags, cy, ccb, ccr);
 }
 
 int jpge_symbol_stats(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
                       const uint8_t qy[64], const uint8_t qc[64], uint32_t counts[1024], uint64_t first[1024],
                       uint32_t flags) {
-    if (!ctx || !rgb || !qy || !qc || !counts || !first) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !counts || !first) return JPGE_E_ARG;
     return ctx->enc->symbol_stats(frame(rgb, w, h, stride, maxval), qy, qc, flags, counts, first);
-}
-
-int jpge_huffman_tables_device(int device, const uint32_t* counts, const uint64_t* first, int nsets, uint32_t* tab,
-                               uint8_t* dht, uint32_t* nsym) {
-    if (!counts || !first || nsets <= 0 || !tab || !dht || !nsym) return JPGE_E_ARG;
-    if (hipSetDevice(device) != hipSuccess) return JPGE_E_HIP;
-    const size_t n = (size_t)nsets * 1024;
-    std::vector<uint64_t> inv(n);
-    for (size_t i = 0; i < n; ++i) inv[i] = ~first[i];  // (K2's global keys are stored inverted)
-    uint32_t *dc = nullptr, *dtab = nullptr, *dn = nullptr;
-    uint64_t* dk = nullptr;
-    uint8_t* dd = nullptr;
-    int st = JPGE_OK;
-    hipStream_t s = nullptr;
-    if (hipStreamCreate(&s) != hipSuccess || hipMalloc((void**)&dc, n * 4) != hipSuccess ||
-        hipMalloc((void**)&dk, n * 8) != hipSuccess || hipMalloc((void**)&dtab, n * 4) != hipSuccess ||
-        hipMalloc((void**)&dd, (size_t)nsets * 4 * jpge::kDhtPiece) != hipSuccess ||
-        hipMalloc((void**)&dn, (size_t)nsets * 16) != hipSuccess) {
-        st = JPGE_E_HIP;
-    } else {
-        jpge::TabArgs a;
-        a.cnt = dc;
-        a.replicas = 1;
-        a.key = dk;
-        a.tab = dtab;
-        a.dht = dd;
-        a.nsym = dn;
-        a.cnt_stride = 1024;
-        a.key_stride = 1024;
-        a.tab_stride = 1024;
-        a.dht_stride = 4 * jpge::kDhtPiece;
-        a.nsym_stride = 4;
-        uint64_t* ddbg = nullptr;
-        const bool stamps = std::getenv("JPGE_HUFFTAB_STAMPS") != nullptr;  // (diagnostic: phase times to stderr)
-        if (stamps && hipMalloc((void**)&ddbg, (size_t)nsets * 4 * 16 * 8) == hipSuccess) {
-            hipMemsetAsync(ddbg, 0, (size_t)nsets * 4 * 16 * 8, s);
-            a.dbg = ddbg;
-        }
-        if (hipMemcpyAsync(dc, counts, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(dk, inv.data(), n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-            jpge::launch_huff_tables(a, (uint32_t)nsets, s) != hipSuccess ||
-            hipMemcpyAsync(tab, dtab, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(dht, dd, (size_t)nsets * 4 * jpge::kDhtPiece, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(nsym, dn, (size_t)nsets * 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            st = JPGE_E_HIP;
-        if (ddbg) {
-            std::vector<uint64_t> h((size_t)nsets * 64);
-            hipMemcpy(h.data(), ddbg, h.size() * 8, hipMemcpyDeviceToHost);
-            for (int i = 0; i < nsets * 4; ++i) {
-                std::fprintf(stderr, "hufftab set %d table %d us:", i / 4, i % 4);
-                for (int k = 1; k < 8; ++k)
-                    std::fprintf(stderr, " %.1f", h[i * 16 + k] ? (double)(h[i * 16 + k] - h[i * 16]) / 100.0 : -1.0);
-                std::fprintf(stderr, "\n");
-            }
-            hipFree(ddbg);
-        }
-    }
-    hipFree(dc);
-    hipFree(dk);
-    hipFree(dtab);
-    hipFree(dd);
-    hipFree(dn);
-    if (s) hipStreamDestroy(s);
-    return st;
 }
 
 int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], uint8_t bits[16],
@@ -373,7 +329,7 @@ int jpge_parse_ppm(const uint8_t* buf, size_t n, uint8_t* rgb, size_t cap, uint3
 }
 
 int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, int quality) {
-    if (!ctx || !ppm_path || !jpg_path) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !ppm_path || !jpg_path) return JPGE_E_ARG;
     jpge::PpmImage img;
     int st = jpge::load_ppm_file(ppm_path, img);
     if (st) return st;
@@ -393,7 +349,7 @@ int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, 
 
 int jpge_encode_files(jpge_ctx* ctx, const char* const* ppm_paths, const char* const* jpg_paths, int n, int quality,
                       size_t* lens, int* statuses, int group) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     return jpge::encode_files(*ctx->enc, ctx->ingest, ppm_paths, jpg_paths, n, quality, lens, statuses, group);
 }
 
@@ -414,7 +370,7 @@ static_assert(sizeof(jpge_stripe_summary) == sizeof(jpge::StripeSummary), "strip
 int jpge_stripe_transform(jpge_ctx* ctx, const uint8_t* rgb, size_t stride, uint32_t width, uint32_t height,
                           uint32_t mcu_row0, uint32_t mcu_rows, int maxval, const uint8_t qy[64],
                           const uint8_t qc[64], int32_t last_dc[3]) {
-    if (!ctx || !rgb || !qy || !qc || !last_dc) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !last_dc) return JPGE_E_ARG;
     jpge::Encoder::StripeDesc d;
     d.rgb = rgb;
     d.stride = stride;
@@ -427,13 +383,13 @@ int jpge_stripe_transform(jpge_ctx* ctx, const uint8_t* rgb, size_t stride, uint
 }
 
 int jpge_stripe_stats(jpge_ctx* ctx, const int32_t seed_dc[3], uint32_t counts[1024], uint64_t first[1024]) {
-    if (!ctx || !seed_dc || !counts || !first) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !seed_dc || !counts || !first) return JPGE_E_ARG;
     return ctx->enc->stripe_stats(seed_dc, counts, first);
 }
 
 int jpge_stripe_code(jpge_ctx* ctx, const uint32_t counts[1024], const uint64_t first[1024],
                      jpge_stripe_summary* summary, size_t* header_len) {
-    if (!ctx || !counts || !first || !summary) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !counts || !first || !summary) return JPGE_E_ARG;
     return ctx->enc->stripe_code(counts, first, reinterpret_cast<jpge::StripeSummary*>(summary), header_len);
 }
 
@@ -445,7 +401,7 @@ int jpge_stripe_place(const jpge_stripe_summary* all, int n, int index, size_t h
 
 int jpge_stripe_pack(jpge_ctx* ctx, const jpge_stripe_summary* all, int n, int index, uint8_t* out, size_t cap,
                      size_t* seg_off, size_t* seg_len, size_t* total_len) {
-    if (!ctx || !all || !out) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || !all || !out) return JPGE_E_ARG;
     return ctx->enc->stripe_pack(reinterpret_cast<const jpge::StripeSummary*>(all), n, index, out, cap, seg_off,
                                  seg_len, total_len);
 }
@@ -457,7 +413,7 @@ extern "C" {
 
 int jpge_color_convert(jpge_ctx* ctx, const double* in0, const double* in1, const double* in2, double* out0,
                        double* out1, double* out2, size_t n, int target, uint32_t flags) {
-    if (!ctx || (target != JPGE_TO_RGB && target != JPGE_TO_YCBCR)) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || (target != JPGE_TO_RGB && target != JPGE_TO_YCBCR)) return JPGE_E_ARG;
     const double* in[3] = {in0, in1, in2};
     double* out[3] = {out0, out1, out2};
     return ctx->enc->stage_color(in, out, n, target == JPGE_TO_YCBCR, flags);
@@ -465,7 +421,7 @@ int jpge_color_convert(jpge_ctx* ctx, const double* in0, const double* in1, cons
 
 int jpge_subsample_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int mode, double* out,
                          uint32_t* out_rows, uint32_t* out_cols, uint32_t flags) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     if (const int e = jpge::Encoder::subsample_shape(mode, rows, cols, out_rows, out_cols)) return e;
     if (!out) return JPGE_OK;
     return ctx->enc->stage_subsample(in, rows, cols, mode, out, flags);
@@ -473,20 +429,20 @@ int jpge_subsample_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_
 
 int jpge_dct_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int dct_mode, double* out,
                    uint32_t flags) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     return ctx->enc->stage_dct(in, rows, cols, dct_mode, out, flags);
 }
 
 int jpge_quantize_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, const uint8_t table[64],
                         int32_t* out, uint32_t flags) {
-    if (!ctx) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc) return JPGE_E_ARG;
     return ctx->enc->stage_quantize(in, rows, cols, table, out, flags);
 }
 
 int jpge_encode_planes(jpge_ctx* ctx, const double* p0, const double* p1, const double* p2, uint32_t rows,
                        uint32_t cols, int colorspace, uint32_t real_width, uint32_t real_height, const uint8_t qy[64],
                        const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len, uint32_t flags) {
-    if (!ctx || (colorspace != JPGE_TO_RGB && colorspace != JPGE_TO_YCBCR)) return JPGE_E_ARG;
+    if (!ctx || !ctx->enc || (colorspace != JPGE_TO_RGB && colorspace != JPGE_TO_YCBCR)) return JPGE_E_ARG;
     const double* p[3] = {p0, p1, p2};
     return ctx->enc->encode_planes(p, rows, cols, colorspace == JPGE_TO_YCBCR, real_width, real_height, qy, qc, out,
                                    cap, len, flags);

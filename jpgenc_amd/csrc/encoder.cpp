@@ -330,6 +330,7 @@ struct Encoder::Slot {
     uint8_t qy[64], qc[64];
     bool timed = false;                // this frame's kernels are bracketed by timing events
     int timed_frames = 1;              // frames those kernels covered (a frame set's launches)
+    bool count_symbols = false;        // a member of a timed launch: its symbols go to times_.symbols
     HistPtrs hist{};                   // this frame's device histograms (in d_ctl)
     uint64_t seq = 0;                  // frame sequence number (handshakes via mapped memory)
     std::atomic<int> tables_done{0};   // set by build_tables (any thread)
@@ -788,6 +789,7 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     if (const int st = prep1(s, f, qy, qc, flags, imp, a, st2)) return st;
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
     s.timed_frames = 1;
+    s.count_symbols = s.timed;
     // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
     const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
     JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
@@ -823,6 +825,7 @@ int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a_in, const Stats
     const uint64_t E = (uint64_t)timing_every_;
     t.timed = E && (c + E - 1) / E * E <= c + (uint64_t)n - 1;  // (a sampled frame number in the set)
     t.timed_frames = n;
+    for (int m = 0; m < n; ++m) s[m]->count_symbols = t.timed;
     const KTimer t1{t.ev[0], t.ev[1]}, t2{t.ev[2], t.ev[3]};
     JPGE_HIP(launch_fdct_set(a, n, t.stream, t.timed ? &t1 : nullptr));
     JPGE_HIP(launch_stats_set(st, n, t.stream, t.timed ? &t2 : nullptr));
@@ -958,7 +961,10 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait) {
         times_.pack_sum += pack;
         times_.frames += s.timed_frames;                       // (the launches' frames)
         times_.launches += 1;
-        times_.symbols += s.symbols * (uint64_t)s.timed_frames;  // (a set: its first member's, for each)
+    }
+    if (s.count_symbols) {  // (every member of a timed set: the launches' record bytes are the sum over them)
+        std::lock_guard<std::mutex> g(times_mu_);
+        times_.symbols += s.symbols;
     }
     if (stamps_file_) hipStreamSynchronize(s.stream);
     dump_stamps(s);
@@ -1809,6 +1815,7 @@ int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_
     s.img_w = real_w;
     s.img_h = real_h;
     s.timed = false;
+    s.count_symbols = false;
     s.tables_done.store(0, std::memory_order_relaxed);
     s.export_queued.store(0, std::memory_order_relaxed);
     // applyDCT(Arai) + applyQuantization (Image.cpp:844-871) into the MCU layout; the

@@ -149,7 +149,8 @@ struct jpge_group {
         }
         return (int)JPGE_OK;
     }
-    ~jpge_group() {
+    // Frees everything; the members' contexts are closed, or at exit released (live.hpp).
+    void release(bool at_exit) {
         for (size_t m = 0; m < dev.size(); ++m) {
             hipSetDevice(dev[m]);
             if (m < xs.size() && xs[m]) hipStreamSynchronize(xs[m]);
@@ -163,9 +164,30 @@ struct jpge_group {
             hipSetDevice(dev[m]);
             if (xs[m]) hipStreamDestroy(xs[m]);
         }
-        for (auto* c : ctx) jpge_close(c);
+        for (auto* c : ctx) {
+            if (at_exit) jpge::live_release(c);
+            else jpge_close(c);
+        }
+        dev.clear();
+        ctx.clear();
+        comm.clear();
+        xs.clear();
+        rgb.clear();
+        out.clear();
+        xb.clear();
+        use_rccl = false;
     }
+    ~jpge_group() { release(false); }
 };
+
+namespace jpge {
+void live_release(jpge_group* g) {  // (the exit handler, capi.cpp)
+    live_remove(g);
+    { std::lock_guard<std::mutex> wait(g->mu); }  // a call still running on another thread
+    g->release(true);
+    live_mark_released(g);
+}
+}  // namespace jpge
 
 extern "C" {
 
@@ -206,13 +228,14 @@ int jpge_group_open(int ndev, const int* devices, int lanes, jpge_group** g) {
 }
 
 int jpge_group_close(jpge_group* g) {
-    if (g) jpge::live_remove(g);
+    if (!g || jpge::live_is_released(g)) return (int)JPGE_OK;  // (released at exit: live.hpp)
+    jpge::live_remove(g);
     delete g;
     return (int)JPGE_OK;
 }
 
 int jpge_group_size(const jpge_group* g, int* n, int* uses_rccl) {
-    if (!g || !n) return (int)JPGE_E_ARG;
+    if (!g || g->dev.empty() || !n) return (int)JPGE_E_ARG;
     *n = (int)g->dev.size();
     if (uses_rccl) *uses_rccl = g->use_rccl ? 1 : 0;
     return (int)JPGE_OK;
@@ -225,7 +248,7 @@ int jpge_group_context(jpge_group* g, int member, jpge_ctx** ctx) {
 }
 
 int jpge_group_set_restart_interval(jpge_group* g, uint32_t mcus) {
-    if (!g) return (int)JPGE_E_ARG;
+    if (!g || g->dev.empty()) return (int)JPGE_E_ARG;
     for (auto* c : g->ctx)
         if (const int st = jpge_set_restart_interval(c, mcus)) return st;
     g->restart = mcus;
@@ -234,7 +257,7 @@ int jpge_group_set_restart_interval(jpge_group* g, uint32_t mcus) {
 
 int jpge_group_encode_batch(jpge_group* g, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
                             uint32_t flags) {
-    if (!g || (n > 0 && !frames) || n < 0) return (int)JPGE_E_ARG;
+    if (!g || g->dev.empty() || (n > 0 && !frames) || n < 0) return (int)JPGE_E_ARG;
     std::lock_guard<std::mutex> lk(g->mu);
     const int N = (int)g->ctx.size();
     std::vector<std::vector<jpge_frame>> part(N);
@@ -254,7 +277,8 @@ int jpge_group_encode_batch(jpge_group* g, jpge_frame* frames, int n, const uint
 int jpge_group_encode_striped(jpge_group* g, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
                               int maxval, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
                               size_t* len) {
-    if (!g || !rgb || !out || !len || !qy || !qc || width == 0 || height == 0) return (int)JPGE_E_ARG;
+    if (!g || g->dev.empty() || !rgb || !out || !len || !qy || !qc || width == 0 || height == 0)
+        return (int)JPGE_E_ARG;
     std::lock_guard<std::mutex> lk(g->mu);
     const int N = (int)g->ctx.size();
     const size_t row = (size_t)width * 3, pitch = stride ? stride : row;

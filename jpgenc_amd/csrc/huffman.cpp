@@ -291,6 +291,58 @@ inline HeapItem heap_pop(HeapItem* h, int& size) {
     return top;
 }
 
+// The same pop restricted to the heap's LIGHT items, every heavier item being the marker
+// kHi (heavier than every weight in use).  When only the pops of the light items are
+// wanted, their order does not depend on the heavy items' weights:
+//  - the hole walks from the root along the lighter child; while a light child exists it
+//    is the lighter one, and once both children are heavy (or absent) the rest of the
+//    walk moves heavy items only;
+//  - the last item v then enters at the bottom of that walk and rises past every heavier
+//    item on it: a heavy v stops below the light items (the walk's exit x becomes heavy),
+//    a light v passes the heavy part and continues from x exactly like a sift-up from x.
+// A push is the same: a light item rises past every heavy ancestor and then by weight; a
+// heavy one never passes a light item, so it is appended as the marker.  So the light
+// items' positions evolve as in the full heap, and the walk stops at the light region's
+// edge (its depth, not the heap's).
+inline HeapItem heap_pop_light(HeapItem* h, int& size, HeapItem heavy) {
+    const HeapItem top = h[0];
+    const int len = size - 1;
+    size = len;
+    if (len <= 0) return top;
+    const HeapItem v = h[len];
+    int hole = 0;
+    const int lim = (len - 1) / 2;
+    for (;;) {
+        if (hole < lim) {  // two children
+            const HeapItem cl = h[2 * hole + 1], cr = h[2 * hole + 2];
+            if ((cl & cr) == heavy) break;  // (both the marker)
+            const bool left = item_hi(cr) > item_hi(cl);
+            const int c = 2 * hole + 2 - (int)left;
+            h[hole] = left ? cl : cr;
+            hole = c;
+        } else {
+            if ((len & 1) == 0 && hole == (len - 2) / 2 && h[2 * hole + 1] != heavy) {
+                h[hole] = h[2 * hole + 1];
+                hole = 2 * hole + 1;
+            }
+            break;
+        }
+    }
+    if (v == heavy) {
+        h[hole] = heavy;
+    } else {
+        const uint32_t vw = item_hi(v);
+        while (hole > 0) {
+            const int parent = (hole - 1) / 2;
+            if (!(item_hi(h[parent]) > vw)) break;
+            h[hole] = h[parent];
+            hole = parent;
+        }
+        h[hole] = v;
+    }
+    return top;
+}
+
 // by_len[l] = the symbols of code length l (l = 1..17) in the reference's order;
 // syms/cnts: the distinct symbols and counts in first-occurrence order.
 void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][kMaxSyms], int nlen[18]) {
@@ -389,12 +441,22 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         }
         return e;
     };
+    // Converged levels.  Once a level's packages weigh exactly what its input packages
+    // weighed (same count, same weights in the same order), the next level is fed the same
+    // weight sequence: the same leaves' heap and the same pushes, so the heap performs the
+    // same moves and pops the same slots.  Its pop order is the previous level's with each
+    // package replaced by its successor (node id + np), and it again produces the same
+    // weights, so every remaining level repeats it.  On 1080p frames 8-9 of the 15 levels.
+    bool converged = false;
     for (int lv = 0; lv < kLevels; ++lv) {
         const HeapItem* in = pk_[lv & 1] + 1;
         HeapItem* out = pk_[(lv + 1) & 1] + 1;
         const int m = n + np, npairs = m / 2;
         int e;
-        if (!wrapped) {
+        if (converged) {
+            for (int k = 0; k < m; ++k) srt[k] += (uint32_t)item_node(srt[k]) >= (uint32_t)n ? (HeapItem)np : 0;
+            e = -1;
+        } else if (!wrapped) {
             // levels[lv] = the leaves + levels[lv-1]'s packages, by weight, leaves first on
             // ties: a branch-free merge run from both ends at once (two independent chains)
             // (one loop body carries both chains: a chain step waits on its loads)
@@ -419,11 +481,24 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         } else {
             e = 2 * npairs - 1;
         }
-        if (e >= 0) {  // the reference's heap up to that tie: the leaves' heap, then the pushes
+        if (e >= 0 && wrapped) {  // the reference's heap: the leaves' heap, then the pushes
             int hn = nbase;
             std::copy(base, base + nbase, heap);
             for (int k = 0; k < np; ++k) heap_push(heap, hn, in[k]);
             for (int k = 0; k <= e; ++k) srt[k] = heap_pop(heap, hn);
+        } else if (e >= 0) {  // the same up to that tie, on its light items (heap_pop_light)
+            const uint32_t wl = item_hi(srt[e]);  // (the tie ends at e: exactly srt[0..e] are light)
+            for (int k = 0; k < nbase; ++k) heap[k] = item_hi(base[k]) > wl ? kHi : base[k];
+            int hn = nbase;
+            for (int k = 0; k < np; ++k) {
+                if (item_hi(in[k]) > wl) {  // (the packages come in weight order: the rest are heavy)
+                    std::fill(heap + hn, heap + hn + (np - k), kHi);
+                    hn += np - k;
+                    break;
+                }
+                heap_push(heap, hn, in[k]);
+            }
+            for (int k = 0; k <= e; ++k) srt[k] = heap_pop_light(heap, hn, kHi);
         }
         for (int k = 0; k < npairs; ++k) {
             const HeapItem a = srt[2 * k], b = srt[2 * k + 1];
@@ -436,6 +511,11 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         }
         out[-1] = kLo;
         out[npairs] = kHi;
+        if (!converged && !wrapped && npairs == np) {
+            uint32_t diff = 0;
+            for (int k = 0; k < np; ++k) diff |= item_hi(out[k]) ^ item_hi(in[k]);
+            converged = diff == 0;
+        }
         np = npairs;
     }
     // levels[15]: levels[14]'s packages alone, pushed in non-decreasing weight, so its
@@ -445,10 +525,15 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     std::copy(fin, fin + np, srt);
     srt[-1] = kLo;
     const int e = wrapped ? np - 1 : last_tie(np, 0);
-    if (e >= 0) {
+    if (e >= 0 && wrapped) {
         int hn = 0;
         for (int k = 0; k < np; ++k) heap_push(heap, hn, fin[k]);
         for (int k = 0; k <= e; ++k) srt[k] = heap_pop(heap, hn);
+    } else if (e >= 0) {
+        const uint32_t wl = item_hi(srt[e]);
+        for (int k = 0; k < np; ++k) heap[k] = item_hi(fin[k]) > wl ? kHi : fin[k];
+        int hn = np;
+        for (int k = 0; k <= e; ++k) srt[k] = heap_pop_light(heap, hn, kHi);
     }
     // Push the multiplicities and the first final package down the DAG (a package's id
     // exceeds its children's).

@@ -158,10 +158,7 @@ constexpr int kTileRecords = kEntropyTile * kRecPerBlock;
 // [j*nb/kRecSub, (j+1)*nb/kRecSub) of the tile, at recs + t*kTileRecords +
 // j*kSubRecords, its count at tcount[t*kRecSub + j].  The code kernel reads a
 // tile's sub-streams in order, so they form the tile's one record stream.
-#ifndef K2_SUB
-#define K2_SUB 4
-#endif
-constexpr int kRecSub = K2_SUB;
+constexpr int kRecSub = 4;
 constexpr int kSubRecords = kTileRecords / kRecSub;
 static_assert(kTileRecords % kRecSub == 0, "sub-streams divide a tile's records");
 
@@ -338,23 +335,6 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
 inline uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) { return seg_layout(g, 0, wgs_override).grid(); }
 
 inline uint64_t entropy_ubuf_bytes(const SegLayout& L) { return (uint64_t)L.grid() * kEntropyRegionBytes; }
-
-// Huffman tables on the device (hufftab.hip): one workgroup per table and histogram
-// set; the same tables as huffman.cpp's build_table, and each table's DHT piece:
-// class/id byte, bits[16] (lengths 1..16), huffval[nsym].
-constexpr int kDhtPiece = 1 + 16 + 256;
-struct TabArgs {
-    const uint32_t* cnt;   // [replicas][4][256] symbol counts (summed over the replicas)
-    uint32_t replicas;
-    const uint64_t* key;   // [4][256] inverted first-occurrence keys (~key; K2's global form)
-    uint32_t* tab;         // [4][256] (len << 16) | code, 0 for absent symbols
-    uint8_t* dht;          // [4][kDhtPiece]
-    uint32_t* nsym;        // [4] symbols per table
-    // per histogram set (grid.y), in elements
-    uint64_t cnt_stride = 0, key_stride = 0, tab_stride = 0, dht_stride = 0, nsym_stride = 0;
-    uint64_t* dbg = nullptr;  // diagnostic phase times: [set][4][16] s_memrealtime stamps
-};
-hipError_t launch_huff_tables(const TabArgs& a, uint32_t sets, hipStream_t s);
 
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t = nullptr);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t = nullptr);

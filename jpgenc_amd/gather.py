@@ -2,103 +2,178 @@
 batch whose frames are dealt over ranks (frame i on rank i mod N) are gathered to
 rank 0, one message per rank.
 
-Each rank packs its frames' bytes back to back in a device buffer with one
-`torch.cat` launch, and sends that run as ONE point-to-point message (RCCL over
-xGMI with the "nccl" backend; gloo in the CPU tests).  The frame lengths travel
-ahead on a host-side gloo group (a few hundred bytes, no device synchronisation), so
-rank 0 posts its receives with exact sizes at exact places: rank r's run lands at
-the sum of the lower ranks' runs, in the order of its frames.
+Each rank packs its frames' bytes back to back with one `torch.cat` launch and moves
+that run to rank 0 in ONE transfer.  Rank 0's batch buffer has a fixed region per rank
+(rank r's run starts at r x cap_bytes), so no rank needs another rank's sizes to know
+where its bytes go.  Two transports:
+  - "p2p": RCCL over xGMI with the "nccl" backend (gloo with CPU tensors in the CPU
+    tests): the run is one isend, matched by an irecv of exactly its size on rank 0;
+  - "ipc": ranks that share one GPU (the --allow-shared-gpu rehearsal; RCCL refuses two
+    ranks on one device): rank 0's batch buffers are opened in every rank through HIP
+    IPC handles, and a rank's cat writes its run straight into its region of them.
+The frame lengths go to rank 0 alone, on a host-side gloo group (a few hundred bytes,
+posted without waiting): rank 0 needs them to size its receives and to find frames;
+the other ranks never wait for anyone's lengths.
 
-`post()` returns as soon as the messages are queued: the next batch's encode runs
-while they move (the encoder's lanes have streams of their own).  Two pack buffers
-alternate; a buffer is reused only after the messages posted from it two batches
-earlier have completed.  Replaces nothing in the reference (a single-process
-encoder); the bytes are the reference's files, unchanged.
+`post()` returns once the transfers are queued (nothing on the host waits for the GPU):
+the next batch's encode runs while they move.  The caller encodes into two sets of
+output slots alternately; `acquire()` names the set to encode into next, after the cat
+that read it two batches earlier has finished (long since, in practice).  Two pack
+and batch buffers alternate the same way.  Replaces nothing in the reference (a
+single-process encoder); the bytes are the reference's files, unchanged.
 """
 from __future__ import annotations
 
+import time
+
 
 class BatchGather:
-    def __init__(self, group, meta_group, rank: int, world: int, nframes: int, cap_bytes: int, device):
-        """group: the data-path group (RCCL, or gloo with CPU tensors); meta_group: a
-        gloo group for the lengths; nframes: the batch; cap_bytes: the largest packed
-        run one rank can send (its frames' capacities summed); device: where the pack
-        buffers live (rank 0's receive buffer too)."""
+    def __init__(self, group, meta_group, rank: int, world: int, nframes: int, cap_bytes: int, device,
+                 transport: str = "p2p"):
+        """group: the data-path group (RCCL, or gloo with CPU tensors; unused by "ipc");
+        meta_group: a gloo group for the lengths; nframes: the batch; cap_bytes: the
+        largest packed run one rank can send (its frames' capacities summed); device:
+        where the pack and batch buffers live; transport: "p2p" or "ipc" (ranks on one
+        GPU; falls back to "p2p" if the IPC handles cannot be opened)."""
         import torch
         import torch.distributed as dist
 
         self.dist, self.torch = dist, torch
         self.group, self.meta = group, meta_group
         self.rank, self.world, self.n = rank, world, nframes
+        self.cap = cap_bytes
         self.nmax = (nframes + world - 1) // world
-        self.packed = [torch.empty(cap_bytes, dtype=torch.uint8, device=device) for _ in range(2)]
-        self.pending = [[], []]  # work handles of the messages posted from each pack buffer
+        self.cuda = torch.device(device).type == "cuda"
+        self.pending = [[], []]   # works posted from each buffer (sends, receives, length messages)
+        self.cat_ev = [None, None]  # the cat that read each output-slot set
         self.turn = 0
-        # rank 0: the whole batch, packed by rank (rank r's run after the runs of ranks < r),
-        # one buffer per pack buffer (a batch's receives never overlap the previous one's)
+        self.last = 0
+        self.where = [None, None]  # rank 0: frame i -> (offset in batch[b], length)
+        self.lens_wait_s = 0.0     # rank 0: host time spent waiting for the other ranks' lengths
+        self.lens_out = [torch.zeros(self.nmax, dtype=torch.int64) for _ in range(2)]
+        self.lens_all = [[torch.zeros(self.nmax, dtype=torch.int64) for _ in range(world)] for _ in range(2)]
+        # rank 0: the batch, rank r's run at r * cap_bytes
         self.batch = [torch.empty(cap_bytes * world if rank == 0 else 1, dtype=torch.uint8, device=device)
                       for _ in range(2)]
-        self.lens_all = [torch.zeros(self.nmax, dtype=torch.int64) for _ in range(world)]
-        self.where = [None, None]  # rank 0: frame i -> (offset in batch[b], length)
-        self.last = 0              # the buffer of the latest post
+        self.transport = "p2p"
+        self.remote = None
+        if transport == "ipc" and self.cuda and world > 1:
+            self.remote = self._open_ipc()
+            if self.remote is not None:
+                self.transport = "ipc"
+        # p2p senders pack into a buffer of their own (rank 0 packs into its region directly)
+        self.packed = [torch.empty(cap_bytes if (rank and self.transport == "p2p") else 1, dtype=torch.uint8,
+                                   device=device) for _ in range(2)]
+
+    def _open_ipc(self):
+        """Every rank opens rank 0's two batch buffers (HIP IPC).  The handles travel over
+        the gloo group; all ranks agree on the outcome, so either all use "ipc" or none."""
+        torch, dist = self.torch, self.dist
+        from torch.multiprocessing.reductions import reduce_tensor
+
+        handles = [[reduce_tensor(t)[1] for t in self.batch] if self.rank == 0 else None]
+        dist.broadcast_object_list(handles, src=dist.get_global_rank(self.meta, 0), group=self.meta)
+        views, ok = None, 1
+        if self.rank == 0:
+            views = self.batch
+        else:
+            try:
+                from torch.multiprocessing.reductions import rebuild_cuda_tensor
+
+                views = [rebuild_cuda_tensor(*h) for h in handles[0]]
+            except Exception:  # (an IPC-less runtime: fall back to p2p)
+                ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.meta)
+        return views if int(flag) == 1 else None
 
     def share(self, r: int) -> list[int]:
         return list(range(r, self.n, self.world))
 
+    def acquire(self) -> int:
+        """The output-slot set (0/1) the caller encodes the next batch into."""
+        ev = self.cat_ev[self.turn]
+        if ev is not None:
+            ev.synchronize()
+            self.cat_ev[self.turn] = None
+        return self.turn
+
     def post(self, segments, lens) -> None:
-        """segments: this rank's frames' byte tensors (length >= lens[k] each), in
-        share order; lens: their .jpg lengths (host ints)."""
+        """segments: this rank's frames' byte tensors (length >= lens[k] each), in share
+        order, from the set acquire() named; lens: their .jpg lengths (host ints)."""
         torch, dist = self.torch, self.dist
         b = self.turn
         self.turn ^= 1
-        for w in self.pending[b]:  # (the messages sent from this buffer two batches ago)
+        for w in self.pending[b]:  # (posted from these buffers two batches ago)
             w.wait()
         self.pending[b] = []
-        mine = torch.zeros(self.nmax, dtype=torch.int64)
-        mine[:len(lens)] = torch.tensor(list(lens), dtype=torch.int64)
-        dist.all_gather(self.lens_all, mine, group=self.meta)
-        total = int(sum(lens))
-        run = self.packed[b][:total]
-        torch.cat([seg[:n] for seg, n in zip(segments, lens)], out=run)
-        if run.is_cuda:  # the caller's next encode rewrites the segments: the pack must be done
+        lens = [int(n) for n in lens]
+        total = sum(lens)
+        if total > self.cap:
+            raise ValueError(f"gather: {total} bytes exceed the rank's region of {self.cap}")
+        meta0 = dist.get_global_rank(self.meta, 0)
+        if self.rank:
+            mine = self.lens_out[b]
+            mine.zero_()
+            if lens:
+                mine[:len(lens)] = torch.tensor(lens, dtype=torch.int64)
+            self.pending[b].append(dist.isend(mine, meta0, group=self.meta))
+        # the run: rank 0 and "ipc" senders cat straight into their region of the batch
+        if self.rank == 0:
+            run = self.batch[b][:total]
+        elif self.transport == "ipc":
+            run = self.remote[b][self.rank * self.cap:self.rank * self.cap + total]
+        else:
+            run = self.packed[b][:total]
+        if total:
+            torch.cat([seg[:n] for seg, n in zip(segments, lens) if n], out=run)
+        if self.cuda:
             ev = torch.cuda.Event()
             ev.record()
-            ev.synchronize()
-        totals = [int(t.sum()) for t in self.lens_all]
+            self.cat_ev[b] = ev
         self.last = b
         if self.rank == 0:
-            ops = []
-            base = totals[0]
-            dst = self.batch[b]
-            dst[:total].copy_(run)
-            for r in range(1, self.world):
-                if totals[r]:
-                    ops.append(dist.P2POp(dist.irecv, dst[base:base + totals[r]],
-                                          dist.get_global_rank(self.group, r), group=self.group))
-                base += totals[r]
-            where = {}
-            base = 0
+            got = self.lens_all[b]
+            waits = [dist.irecv(got[r], dist.get_global_rank(self.meta, r), group=self.meta)
+                     for r in range(1, self.world)]
+            t0 = time.perf_counter()
+            for w in waits:
+                w.wait()
+            self.lens_wait_s += time.perf_counter() - t0
+            got[0].zero_()
+            if lens:
+                got[0][:len(lens)] = torch.tensor(lens, dtype=torch.int64)
+            where, ops = {}, []
             for r in range(self.world):
-                off = base
+                off = r * self.cap
                 for k, i in enumerate(self.share(r)):
-                    n = int(self.lens_all[r][k])
+                    n = int(got[r][k])
                     where[i] = (off, n)
                     off += n
-                base += totals[r]
+                tot = off - r * self.cap
+                if r and tot and self.transport == "p2p":
+                    ops.append(dist.P2POp(dist.irecv, self.batch[b][r * self.cap:r * self.cap + tot],
+                                          dist.get_global_rank(self.group, r), group=self.group))
             self.where[b] = where
         else:
-            ops = [dist.P2POp(dist.isend, run, dist.get_global_rank(self.group, 0), group=self.group)] if total else []
+            ops = [dist.P2POp(dist.isend, run, dist.get_global_rank(self.group, 0), group=self.group)] \
+                if total and self.transport == "p2p" else []
         if ops:
-            self.pending[b] = dist.batch_isend_irecv(ops)
+            self.pending[b] += dist.batch_isend_irecv(ops)
 
     def wait(self) -> None:
-        """Every posted message complete (rank 0: `batch` holds the last batch)."""
+        """Every posted transfer complete (rank 0: `batch` holds the last batch once every
+        rank has returned from wait(), e.g. after a barrier)."""
         for b in (0, 1):
             for w in self.pending[b]:
                 w.wait()
             self.pending[b] = []
+            if self.cat_ev[b] is not None:
+                self.cat_ev[b].synchronize()
+        if self.cuda:
+            self.torch.cuda.current_stream().synchronize()
 
     def frame(self, i: int):
-        """Rank 0, after wait(): frame i's .jpg bytes in the latest batch (a view)."""
+        """Rank 0, after wait() on every rank: frame i's .jpg bytes in the latest batch (a view)."""
         off, n = self.where[self.last][i]
         return self.batch[self.last][off:off + n]

@@ -129,7 +129,7 @@ def test_batch_share_deals_every_frame_once():
     assert bench.batch_seed(0) == 1000  # config 4 seeds
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world, port, q, B=37):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
@@ -139,7 +139,7 @@ def _gather_worker(rank, world, port, q):
     from jpgenc_amd.gather import BatchGather
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    B, cap = 37, 300  # a batch that does not divide over the ranks; some empty segments
+    cap = 300  # (B: a batch that does not divide over the ranks; some empty segments)
     g = BatchGather(dist.new_group(backend="gloo"), dist.new_group(backend="gloo"), rank, world, B,
                     ((B + world - 1) // world) * cap, "cpu")
 
@@ -158,6 +158,8 @@ def _gather_worker(rank, world, port, q):
             seg[:len(b)] = b
             segs.append(seg)
             lens.append(len(b))
+        s = g.acquire()
+        assert s == step % 2
         g.post(segs, lens)
         if rank == 0:
             g.wait()
@@ -168,16 +170,17 @@ def _gather_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world", [2, 3])
-def test_batch_gather_is_byte_equal(world):
+@pytest.mark.parametrize("world,B", [(2, 37), (3, 37), (3, 2)])
+def test_batch_gather_is_byte_equal(world, B):
     """Config 4's gather: each rank packs its frames' bytes into one
     message; rank 0 finds every frame of the batch byte-equal, over three batches
-    (both pack buffers used, one reused)."""
+    (both pack buffers used, one reused).  B=2 over 3 ranks: a rank with no frames
+    (ADVICE r4)."""
     mp = pytest.importorskip("torch.multiprocessing")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, B)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=150) for _ in procs)

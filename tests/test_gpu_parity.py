@@ -178,12 +178,15 @@ def test_entropy_scan_kernel_placement(in_code, wgs, w, h, kind, quality):
 # The largest grid placed by the code kernel's last workgroup (kPlaceInCodeMaxWgs = 4096
 # entropy workgroups, an 8K frame's 6 075 tiles over 4 096 workgroups): that path relies
 # on gfx950's write-through record stores plus vmcnt(0) before the completion count
-# (kernels.hpp), so it is pinned at its maximum size.
-def test_placement_in_code_at_max_grid():
+# (kernels.hpp), so it is pinned at its maximum size on flat
+# data and on dense data (photo-like and random frames at Q100, where
+# every workgroup writes many records, so a stale record would show).
+@pytest.mark.parametrize("kind,quality", [(2, 90), (0, 100), (1, 100)])
+def test_placement_in_code_at_max_grid(kind, quality):
     enc = _encoder_with_env(JPGE_ENTROPY_WGS=4096, JPGE_EXT_PLACE=1, JPGE_PLACE_IN_CODE=1)
     try:
-        rgb = J.synth_rgb8(8081, 7680, 4320, kind=2)
-        assert enc.encode(rgb, quality=90) == _oracle.encode(rgb, 90)
+        rgb = J.synth_rgb8(8081 + kind, 7680, 4320, kind=kind)
+        assert enc.encode(rgb, quality=quality) == _oracle.encode(rgb, quality)
     finally:
         enc.close()
 

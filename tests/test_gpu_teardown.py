@@ -48,3 +48,16 @@ def test_exit_with_open_encoder_and_groups(mode):
     if mode == "end":
         assert "ok" in r.stdout
     assert "Segmentation" not in out and "Aborted" not in out, out[-3000:]
+
+
+@pytest.mark.gpu
+def test_caller_close_after_library_exit_handler():
+    """a C caller whose atexit cleanup was registered before jpge_open closes
+    its context and group after the library released them at exit: no-ops, no double
+    free; other calls on the released handles return JPGE_E_ARG."""
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", "test_exit_close")
+    assert os.path.exists(exe), "build with make"
+    r = subprocess.run([exe], cwd=ROOT, capture_output=True, text=True, timeout=110)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, f"rc {r.returncode}\n{out[-3000:]}"
+    assert "encoded" in r.stdout and "cleanup ok" in r.stdout, out[-3000:]
