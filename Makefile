@@ -17,7 +17,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -pthread -Wall -Wextra -Wno-unused-parameter -W
 
 HOST_SRCS := encoder.cpp capi.cpp host_io.cpp huffman.cpp jpge_image.cpp ingest.cpp host_decode.cpp coding.cpp group.cpp
 HOST_OBJS := $(addprefix $(BUILD)/,$(HOST_SRCS:.cpp=.o))
-DEV_SRCS  := fdct.hip stats.hip entropy.hip planes.hip
+DEV_SRCS  := fdct.hip stats.hip entropy.hip planes.hip concat.hip
 DEV_OBJS  := $(addprefix $(BUILD)/,$(DEV_SRCS:.hip=.o))
 DIAG_OBJS := $(addprefix $(BUILD)/diag/,$(DEV_SRCS:.hip=.o))
 HEADERS   := $(wildcard $(SRC)/*.hpp) include/jpge.h

@@ -171,6 +171,16 @@ int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], ui
  * tools): writes n distinct symbols as (symbol, length, code) in DHT order. */
 int jpge_huffman_text(const int* text, size_t n, int* syms, int* lens, uint32_t* codes, int* nsym);
 
+/* Concatenate n device byte segments (segs[k], lens[k] bytes) back to back into the
+ * device buffer dst, in one kernel launch per 96 segments on `stream` (a hipStream_t;
+ * NULL = the null stream), without waiting for it; *total (optional) = the sum of the
+ * lengths.  device: the GPU the buffers live on (the caller's current device is kept).
+ * Config 4's gather packs a rank's .jpg bytes with it (jpgenc_amd/gather.py) before
+ * the one transfer to rank 0.  Replaces nothing in the reference (its encoder is one
+ * process); an addition of this library.  Any alignments; segments below 2 GB. */
+int jpge_concat_segments(int device, void* stream, const uint8_t* const* segs, const size_t* lens, int n,
+                         uint8_t* dst, size_t* total);
+
 /* ---- Decode-side verification utilities (host) ---- */
 
 /* huffmanDecode (Huffman.hpp:62, Huffman.cpp:91-146): the symbol text coded in the

@@ -46,7 +46,7 @@ EXPORTS = (
     "jpge_encode_category", "jpge_dc_difference", "jpge_color_convert", "jpge_subsample_plane", "jpge_dct_plane",
     "jpge_quantize_plane", "jpge_encode_planes",
     "jpge_group_open", "jpge_group_close", "jpge_group_size", "jpge_group_context", "jpge_group_set_restart_interval",
-    "jpge_group_encode_batch", "jpge_group_encode_striped",
+    "jpge_group_encode_batch", "jpge_group_encode_striped", "jpge_concat_segments",
 )
 
 JPGE_TO_RGB, JPGE_TO_YCBCR = 0, 1
@@ -142,6 +142,7 @@ def lib() -> ctypes.CDLL:
         L.jpge_stripe_pack.argtypes = [vp, ctypes.POINTER(StripeSummary), i32, i32, vp, sz, ctypes.POINTER(sz),
                                        ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.jpge_huffman_table.argtypes = [vp, vp, vp, vp, ctypes.POINTER(i32), vp, vp]
+        L.jpge_concat_segments.argtypes = [i32, vp, vp, vp, i32, vp, ctypes.POINTER(sz)]
         L.jpge_huffman_text.argtypes = [vp, sz, vp, vp, vp, ctypes.POINTER(i32)]
         L.jpge_parse_ppm.argtypes = [vp, sz, vp, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
                                      ctypes.POINTER(i32)]
@@ -284,6 +285,22 @@ def decode_coeffs(data: bytes):
     _check(lib().jpge_decode_coeffs(_p(buf), buf.size, ctypes.byref(info), _p(y), _p(cb), _p(cr), y.shape[0],
                                     cb.shape[0]), "decode_coeffs")
     return info, y, cb, cr
+
+
+def concat_segments(device: int, stream: int, ptrs, lens, dst: int) -> int:
+    """jpge_concat_segments: device byte runs (pointers ptrs[k], lens[k] bytes) back to
+    back into the device buffer dst, queued on `stream` (a hipStream_t as an int, 0 =
+    the null stream).  ptrs/lens may be ctypes arrays (reused) or sequences.  Returns
+    the total length."""
+    n = len(ptrs)
+    if not isinstance(ptrs, ctypes.Array):
+        ptrs = (ctypes.c_void_p * n)(*ptrs)
+    if not isinstance(lens, ctypes.Array):
+        lens = (ctypes.c_size_t * n)(*lens)
+    tot = ctypes.c_size_t()
+    _check(lib().jpge_concat_segments(int(device), stream or None, ptrs, lens, n, dst, ctypes.byref(tot)),
+           "concat_segments")
+    return tot.value
 
 
 def huffman_table(counts, first):

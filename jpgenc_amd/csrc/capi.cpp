@@ -276,6 +276,37 @@ int jpge_symbol_stats(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h,
     return ctx->enc->symbol_stats(frame(rgb, w, h, stride, maxval), qy, qc, flags, counts, first);
 }
 
+int jpge_concat_segments(int device, void* stream, const uint8_t* const* segs, const size_t* lens, int n,
+                         uint8_t* dst, size_t* total) {
+    if (n < 0 || (n > 0 && (!segs || !lens || !dst))) return JPGE_E_ARG;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) return JPGE_E_HIP;
+    if (prev != device && hipSetDevice(device) != hipSuccess) return JPGE_E_NODEV;
+    int st = JPGE_OK;
+    uint64_t off = 0;
+    for (int k0 = 0; k0 < n && st == JPGE_OK; k0 += (int)jpge::kConcatMax) {
+        jpge::ConcatArgs a;
+        a.dst = dst;
+        a.n = (uint32_t)std::min<int>(n - k0, (int)jpge::kConcatMax);
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < a.n; ++k) {
+            if (lens[k0 + k] && !segs[k0 + k]) { st = JPGE_E_ARG; break; }
+            a.src[k] = segs[k0 + k];
+            a.len[k] = lens[k0 + k];
+            a.off[k] = off;
+            a.chunk0[k] = c;
+            c += jpge::concat_chunks(a.len[k], reinterpret_cast<uintptr_t>(dst + off));
+            off += a.len[k];
+        }
+        a.chunk0[a.n] = c;
+        if (st == JPGE_OK && jpge::launch_concat(a, c, static_cast<hipStream_t>(stream)) != hipSuccess)
+            st = JPGE_E_HIP;
+    }
+    if (total) *total = (size_t)off;
+    if (prev != device) hipSetDevice(prev);
+    return st;
+}
+
 int jpge_huffman_table(const uint32_t counts[256], const uint64_t first[256], uint8_t bits[16],
                        uint8_t huffval[256], int* nsym, uint32_t code[256], uint8_t len[256]) {
     if (!counts || !first || !bits || !huffval || !nsym || !code || !len) return JPGE_E_ARG;

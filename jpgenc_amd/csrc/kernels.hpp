@@ -336,6 +336,20 @@ inline uint32_t entropy_grid(const Geometry& g, uint32_t wgs_override) { return 
 
 inline uint64_t entropy_ubuf_bytes(const SegLayout& L) { return (uint64_t)L.grid() * kEntropyRegionBytes; }
 
+// Segment concatenation (concat.hip): segment k's len[k] bytes from src[k] to dst + off[k];
+// workgroups [chunk0[k], chunk0[k+1]) copy segment k (concat_chunks(len, dst + off) each)
+constexpr uint32_t kConcatMax = 96;  // segments per launch (the arguments stay under 4 KB)
+struct ConcatArgs {
+    uint8_t* dst;
+    uint32_t n;
+    uint32_t chunk0[kConcatMax + 1];
+    const uint8_t* src[kConcatMax];
+    uint64_t off[kConcatMax];
+    uint64_t len[kConcatMax];
+};
+uint32_t concat_chunks(uint64_t len, uintptr_t dst);
+hipError_t launch_concat(const ConcatArgs& a, uint32_t nchunks, hipStream_t s);
+
 hipError_t launch_fdct(const FdctArgs& a, hipStream_t s, const KTimer* t = nullptr);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t = nullptr);
 // frame sets (kMaxSet frames of one geometry, one launch per kernel): the members'

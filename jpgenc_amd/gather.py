@@ -2,7 +2,7 @@
 batch whose frames are dealt over ranks (frame i on rank i mod N) are gathered to
 rank 0, one message per rank.
 
-Each rank packs its frames' bytes back to back with one `torch.cat` launch and moves
+Each rank packs its frames' bytes back to back with one kernel launch and moves
 that run to rank 0 in ONE transfer.  Rank 0's batch buffer has a fixed region per rank
 (rank r's run starts at r x cap_bytes), so no rank needs another rank's sizes to know
 where its bytes go.  Two transports:
@@ -11,7 +11,9 @@ where its bytes go.  Two transports:
   - "ipc": ranks that share one GPU (the --allow-shared-gpu rehearsal; RCCL refuses two
     ranks on one device): rank 0's batch buffers are opened in every rank through HIP
     IPC handles, and a rank's cat writes its run straight into its region of them.
-The frame lengths go to rank 0 alone, on a host-side gloo group (a few hundred bytes,
+The pack is one jpge_concat_segments launch (a HIP kernel, any byte alignment) on the
+caller's current stream; CPU tensors (the gloo tests) use torch.cat.  The frame
+lengths go to rank 0 alone, on a host-side gloo group (a few hundred bytes,
 posted without waiting): rank 0 needs them to size its receives and to find frames;
 the other ranks never wait for anyone's lengths.
 
@@ -24,6 +26,7 @@ single-process encoder); the bytes are the reference's files, unchanged.
 """
 from __future__ import annotations
 
+import ctypes
 import time
 
 
@@ -48,7 +51,12 @@ class BatchGather:
         self.cat_ev = [None, None]  # the cat that read each output-slot set
         self.turn = 0
         self.last = 0
-        self.where = [None, None]  # rank 0: frame i -> (offset in batch[b], length)
+        self.got = [None, None]    # rank 0: every rank's lengths of the batch in buffer b
+        self.where = [None, None]  # rank 0: frame offsets in batch[b] (built on first use)
+        self._ptrs = {}            # id(segment list) -> (the list, its device pointers as a ctypes array)
+        self.dev_index = torch.device(device).index if self.cuda else None
+        if self.cuda and self.dev_index is None:
+            self.dev_index = torch.cuda.current_device()
         self.lens_wait_s = 0.0     # rank 0: host time spent waiting for the other ranks' lengths
         self.lens_out = [torch.zeros(self.nmax, dtype=torch.int64) for _ in range(2)]
         self.lens_all = [[torch.zeros(self.nmax, dtype=torch.int64) for _ in range(world)] for _ in range(2)]
@@ -125,7 +133,16 @@ class BatchGather:
             run = self.remote[b][self.rank * self.cap:self.rank * self.cap + total]
         else:
             run = self.packed[b][:total]
-        if total:
+        if total and self.cuda:
+            from . import concat_segments
+
+            key = id(segments)
+            hit = self._ptrs.get(key)
+            if hit is None or hit[0] is not segments:
+                hit = self._ptrs[key] = (segments, (ctypes.c_void_p * len(segments))(*[t.data_ptr() for t in segments]))
+            concat_segments(self.dev_index, torch.cuda.current_stream().cuda_stream, hit[1],
+                            (ctypes.c_size_t * len(lens))(*lens), run.data_ptr())
+        elif total:
             torch.cat([seg[:n] for seg, n in zip(segments, lens) if n], out=run)
         if self.cuda:
             ev = torch.cuda.Event()
@@ -143,18 +160,15 @@ class BatchGather:
             got[0].zero_()
             if lens:
                 got[0][:len(lens)] = torch.tensor(lens, dtype=torch.int64)
-            where, ops = {}, []
-            for r in range(self.world):
-                off = r * self.cap
-                for k, i in enumerate(self.share(r)):
-                    n = int(got[r][k])
-                    where[i] = (off, n)
-                    off += n
-                tot = off - r * self.cap
-                if r and tot and self.transport == "p2p":
-                    ops.append(dist.P2POp(dist.irecv, self.batch[b][r * self.cap:r * self.cap + tot],
-                                          dist.get_global_rank(self.group, r), group=self.group))
-            self.where[b] = where
+            ops = []
+            if self.transport == "p2p":
+                for r in range(1, self.world):
+                    tot = int(got[r].sum())
+                    if tot:
+                        ops.append(dist.P2POp(dist.irecv, self.batch[b][r * self.cap:r * self.cap + tot],
+                                              dist.get_global_rank(self.group, r), group=self.group))
+            self.got[b] = got
+            self.where[b] = None
         else:
             ops = [dist.P2POp(dist.isend, run, dist.get_global_rank(self.group, 0), group=self.group)] \
                 if total and self.transport == "p2p" else []
@@ -175,5 +189,9 @@ class BatchGather:
 
     def frame(self, i: int):
         """Rank 0, after wait() on every rank: frame i's .jpg bytes in the latest batch (a view)."""
-        off, n = self.where[self.last][i]
-        return self.batch[self.last][off:off + n]
+        b = self.last
+        if self.where[b] is None:  # (frame i = share(i mod world)[i div world])
+            self.where[b] = [[0] + [int(x) for x in self.got[b][r].cumsum(0)] for r in range(self.world)]
+        r, k = i % self.world, i // self.world
+        off = r * self.cap + self.where[b][r][k]
+        return self.batch[b][off:off + self.where[b][r][k + 1] - self.where[b][r][k]]
