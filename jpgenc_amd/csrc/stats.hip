@@ -127,6 +127,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     const uint32_t shl = (uint32_t)(64 - lane) & 63u;
     const uint64_t lanes_ac = ~1ull;  // every lane but the DC
     const uint32_t dc_tab = lane == 0 ? 1u << 24 : 0u;  // (a record's table byte: 2t + 1 -> 2t)
+    const uint32_t dc_word = lane == 0 ? 0u - 16u : 0u;  // (a counter word: the DC table's is the AC table's - 16)
     int16_t* st16 = reinterpret_cast<int16_t*>(L.stage[wv]);
     uint4* st4 = reinterpret_cast<uint4*>(L.stage[wv]);
 
@@ -189,8 +190,6 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             dd = (int)(int16_t)dcv - (int)(int16_t)pd;
         }
         if (sn < ns) load_dcs(sn);
-        const int dcat = __builtin_amdgcn_frexp_expf((float)dd);
-        const uint32_t drec = rec_word(2u * tsel, (uint32_t)dcat, extra_bits(dd, dcat));
         if (si == (uint32_t)wv) JPGE_STAMP(1);  // (wave 0: its first sub-stream's data is in)
         JPGE_ACC(1, tq);
 
@@ -200,7 +199,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         uint32_t base = 0;   // the block's first record (its DC) in the sub-stream
         // one block's fields (lane p: zig-zag position p)
         struct Blk {
-            uint64_t M, em;     // AC non-zeros; the lanes with a record (+ lane 63: non-zero, or the EOB)
+            uint64_t M, em;     // AC non-zeros; the lanes with a record (lane 0: the DC; lane 63: non-zero, or the EOB)
             uint32_t rk, run;   // record index in the block (DC = 0), zeros before the coefficient
             uint32_t rec, w;    // the record; its counter / key word
             uint32_t Tj, acbj, acw;  // the block's AC table (top byte), key base, table base word
@@ -220,13 +219,15 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             const uint32_t bits = extra_bits(c, cat);
             const uint32_t rr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? (b.run & 15u) : 0u;  // (the EOB lane, the DC lane: 0)
             // lane 0 (the DC position, where the stage holds the block's DC difference)
-            // codes the block's DC record (its table: the AC table's number less one),
-            // stored with the block's other records at its first record (rank 0): stored
-            // after the sub-stream, the DC records rewrote lines already written back (K2
-            // wrote 1.24x its record bytes)
+            // codes the block's DC symbol like an AC lane: its record (its table: the AC
+            // table's number less one) at the block's first record (rank 0), its count in
+            // the DC table's word (16 below the AC table's first), its key as text index
+            // * 128 + 1 (the flush divides it back).  Stored after the sub-stream, the DC
+            // records had rewritten lines already written back (K2 wrote 1.24x its record
+            // bytes); counted after the sub-stream, they cost a pass of their own.
             b.rec = (b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits) ^ dc_tab;
-            b.w = b.acw + (uint32_t)cat + kRunStride * rr;
-            b.em = b.M | (1ull << 63);
+            b.w = b.acw + (uint32_t)cat + (kRunStride * rr + dc_word);
+            b.em = B1 | (1ull << 63);
             b.zrl = (__ballot(b.run >= 16u) & b.M) != 0;
             return b;
         };
@@ -248,14 +249,13 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                     if (kz < L.key[wz]) atomicMin(&L.key[wz], kz);
                 }
             }
-            if (lane == 0) srec[base] = b.rec;  // (the DC record)
             if (__builtin_amdgcn_inverse_ballot_w64(b.em)) {
                 srec[base + b.rk] = b.rec;
                 atomicAdd(&cnt[b.w], 1u);
                 const uint32_t kk = b.acbj + k2p;
                 if (kk < L.key[b.w]) atomicMin(&L.key[b.w], kk);
             }
-            return 1u + (uint32_t)__builtin_popcountll(b.em) + zt;  // DC, the non-zeros and the EOB, the ZRLs
+            return (uint32_t)__builtin_popcountll(b.em) + zt;  // DC, the non-zeros and the EOB, the ZRLs
         };
 #pragma unroll
         for (int ch = 0; ch < kWRows; ++ch) {  // 8-block chunks: stage one, load the next sub-stream's into its registers
@@ -284,23 +284,25 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 if (!(A.zrl || B.zrl)) {
                     // lanes without a record store out of range (dropped); their counter adds
                     // are masked off
-                    baseB = base + 1u + (uint32_t)__builtin_popcountll(A.em);
+                    baseB = base + (uint32_t)__builtin_popcountll(A.em);
                     const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
-                    // (lane 0: the DC record, at rank 0)
-                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia || lane == 0 ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib || lane == 0 ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
                     if (ia) atomicAdd(&cnt[A.w], 1u);
                     if (ib) atomicAdd(&cnt[B.w], 1u);
                     // (every lane reads its word: a lane without a record has c = 0, so its
                     // word is its table's first, and lane 0's is in range too)
                     const uint32_t kvA = L.key[A.w], kvB = L.key[B.w];
                     const uint32_t kkA = A.acbj + k2p, kkB = B.acbj + k2p;
-                    const bool fa = ia && kkA < kvA, fb = ib && kkB < kvB;
-                    if (__ballot(fa || fb)) {  // (rare: a first occurrence in this workgroup so far)
-                        if (fa) atomicMin(&L.key[A.w], kkA);
-                        if (fb) atomicMin(&L.key[B.w], kkB);
+                    // (rare: a first occurrence in this workgroup so far; the masks of the
+                    // compares, which a bool's ballot would rebuild lane by lane)
+                    const uint64_t fA = A.em & __builtin_amdgcn_ballot_w64(kkA < kvA);
+                    const uint64_t fB = B.em & __builtin_amdgcn_ballot_w64(kkB < kvB);
+                    if (fA | fB) {
+                        if (__builtin_amdgcn_inverse_ballot_w64(fA)) atomicMin(&L.key[A.w], kkA);
+                        if (__builtin_amdgcn_inverse_ballot_w64(fB)) atomicMin(&L.key[B.w], kkB);
                     }
-                    base = baseB + 1u + (uint32_t)__builtin_popcountll(B.em);
+                    base = baseB + (uint32_t)__builtin_popcountll(B.em);
                 } else {
                     baseB = base + emit(A, base);
                     base = baseB + emit(B, baseB);
@@ -309,12 +311,6 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             if (jb < j1) base += emit(prep(cnA, jb), base);  // an odd last block
         }
         JPGE_ACC(2, tq);
-        if ((uint32_t)lane < nb) {  // the DC symbols' counts and keys (their records went with their blocks)
-            const uint32_t w = ((drec >> 25) ? tab_base(2) : tab_base(0)) + ((drec >> 16) & 0xFFu);
-            const uint32_t rk = (acb & 0x80000000u) | ((acb & 0x7FFFFFFFu) >> 7);  // the text index
-            atomicAdd(&cnt[w], 1u);
-            if (rk < L.key[w]) atomicMin(&L.key[w], rk);
-        }
         if (lane == 0) a.tcount[s] = base;
         si = sn;
         JPGE_ACC(3, tq);
@@ -337,7 +333,8 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         uint64_t kb;  // (global texts: a stripe's bases are offset into the whole image)
         if (t < 2) kb = a.key_y0 + ybase;
         else kb = a.key_c0 + cbase + ((k32 & 0x80000000u) ? ncb : 0ull);
-        const uint64_t gkey = ((t & 1) ? kb * 128ull : kb) + (k32 & 0x7FFFFFFFu);
+        // (AC keys: text index * 128 + 2p + delta; DC keys were kept as text index * 128 + 1)
+        const uint64_t gkey = (t & 1) ? kb * 128ull + (k32 & 0x7FFFFFFFu) : kb + ((k32 & 0x7FFFFFFFu) >> 7);
         const unsigned long long inv = ~gkey;
         unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[i]);
         if (inv > *gk) atomicMax(gk, inv);
