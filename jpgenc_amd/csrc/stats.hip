@@ -10,6 +10,7 @@
 // key is stored inverted so atomicMax keeps the minimum.
 #include <algorithm>
 #include <cstddef>
+#include <type_traits>
 
 #include "device_common.hpp"
 
@@ -55,9 +56,15 @@ constexpr int kWCopies = 8;  // LDS counter copies (lane & 7)
 // (a stride of 16 put runs 0 and 2, or 1 and 3, of a size on one bank), and is
 // injective for sizes up to 18.
 constexpr uint32_t kRunStride = 19;
+// A component's DC table follows its AC table at kRunStride * 16 words (run 16 of the
+// AC layout), so lane 0 (the DC position) reaches it through the same word formula
+// with a run of 16.
 constexpr uint32_t kAcWords = 15 + kRunStride * 15 + 1;  // 301
-__host__ __device__ constexpr uint32_t tab_base(uint32_t t) { return (t >> 1) * (16 + kAcWords) + (t & 1) * 16; }
-constexpr uint32_t kWSyms = tab_base(3) + kAcWords;  // 634 words: Y-DC, Y-AC, C-DC, C-AC
+constexpr uint32_t kDcOff = kRunStride * 16;             // 304
+constexpr uint32_t kCompWords = kDcOff + 16;             // 320: Y (AC, DC), then C
+static_assert(kAcWords <= kDcOff, "the DC table after the AC words");
+__host__ __device__ constexpr uint32_t tab_base(uint32_t t) { return (t >> 1) * kCompWords + ((t & 1) ? 0 : kDcOff); }
+constexpr uint32_t kWSyms = 2 * kCompWords;  // 640 words
 // copy stride == 32 / copies (mod 32): the copies of a word sit on distinct banks
 constexpr uint32_t kWBankStep = 32u / kWCopies;
 constexpr uint32_t kWCopyWords = (kWSyms + 64 + 31 - kWBankStep) / 32 * 32 + kWBankStep;
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     const uint32_t shl = (uint32_t)(64 - lane) & 63u;
     const uint64_t lanes_ac = ~1ull;  // every lane but the DC
     const uint32_t dc_tab = lane == 0 ? 1u << 24 : 0u;  // (a record's table byte: 2t + 1 -> 2t)
-    const uint32_t dc_word = lane == 0 ? 0u - 16u : 0u;  // (a counter word: the DC table's is the AC table's - 16)
+    const uint32_t dc_run = lane == 0 ? 16u : 0u;  // (lane 0's run: its counter word is the DC table's, kDcOff)
     int16_t* st16 = reinterpret_cast<int16_t*>(L.stage[wv]);
     uint4* st4 = reinterpret_cast<uint4*>(L.stage[wv]);
 
@@ -143,8 +150,8 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     };
     auto load_dcs = [&](uint32_t si) {
         const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
-        const int64_t g = (int64_t)b0 - 6 + lane;
-        dcs = ((uint32_t)lane < nb + 6 && g >= 0) ? a.coef[(uint64_t)g * 64] : 0;
+        const int32_t g = (int32_t)(b0 + (uint32_t)lane) - 6;  // (block numbers < 2^25: launch_stats)
+        dcs = ((uint32_t)lane < nb + 6 && g >= 0) ? a.coef[(uint64_t)(uint32_t)g * 64] : 0;
     };
     uint32_t si = (uint32_t)wv;
     if (si < ns) {
@@ -205,7 +212,13 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             uint32_t Tj, acbj, acw;  // the block's AC table (top byte), key base, table base word
             bool zrl;           // a run of 16+ zeros before a non-zero
         };
-        auto prep = [&](int c, uint32_t jb) {
+        // kExact: runs exact (every length; the ZRL path).  Otherwise exact up to 31:
+        // the leading zeros of the 32 mask bits below p, with a 1 below them (a window
+        // without a non-zero, a run of 32+, reads 31); a block with a run of 16+ takes
+        // the ZRL path, which recomputes it exactly, so the fast path codes runs < 16
+        // and needs no mask of the run's low 4 bits.
+        auto prep = [&](int c, uint32_t jb, auto exact) {
+            constexpr bool kExact = decltype(exact)::value;
             Blk b;
             const uint64_t B1 = __ballot(c != 0) | 1ull;  // the AC non-zeros, and bit 0
             b.M = B1 & lanes_ac;
@@ -214,26 +227,30 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             b.acw = twj & 0xFFFFu;                          // its first counter / key word
             b.acbj = __builtin_amdgcn_readlane(acb, jb);    // (+ 2p: the key; the EOB lane 63: text * 128 + 127)
             b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0u));
-            b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
+            if constexpr (kExact) b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
+            else b.run = (uint32_t)__builtin_clz((uint32_t)((B1 << shl) >> 32) | 1u);
             const int cat = __builtin_amdgcn_frexp_expf((float)c);
             const uint32_t bits = extra_bits(c, cat);
-            const uint32_t rr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? (b.run & 15u) : 0u;  // (the EOB lane, the DC lane: 0)
+            // (the EOB lane: 0; the DC lane: 16)
+            const uint32_t rr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? (kExact ? b.run & 15u : b.run) : dc_run;
             // lane 0 (the DC position, where the stage holds the block's DC difference)
             // codes the block's DC symbol like an AC lane: its record (its table: the AC
-            // table's number less one) at the block's first record (rank 0), its count in
-            // the DC table's word (16 below the AC table's first), its key as text index
-            // * 128 + 1 (the flush divides it back).  Stored after the sub-stream, the DC
-            // records had rewritten lines already written back (K2 wrote 1.24x its record
-            // bytes); counted after the sub-stream, they cost a pass of their own.
+            // table's number less one; the run of 16 sets a bit the table byte has) at the
+            // block's first record (rank 0), its count in the DC table's word (kDcOff past
+            // the AC table's first), its key as text index * 128 + 1 (the flush divides
+            // it back).  Stored after the sub-stream, the DC records had rewritten lines
+            // already written back (K2 wrote 1.24x its record bytes); counted after the
+            // sub-stream, they cost a pass of their own.
             b.rec = (b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits) ^ dc_tab;
-            b.w = b.acw + (uint32_t)cat + (kRunStride * rr + dc_word);
+            b.w = b.acw + (uint32_t)cat + kRunStride * rr;
             b.em = B1 | (1ull << 63);
             b.zrl = (__ballot(b.run >= 16u) & b.M) != 0;
             return b;
         };
-        // (general form, every block with ZRLs) its records from `base`, histogram and
-        // keys; returns its record count
-        auto emit = [&](Blk b, uint32_t base) -> uint32_t {
+        // (general form, every block with ZRLs) block jb's records from `base`, histogram
+        // and keys, all from its staged coefficient c; returns its record count
+        auto emit = [&](int c, uint32_t jb, uint32_t base) -> uint32_t {
+            Blk b = prep(c, jb, std::true_type{});
             uint32_t zt = 0;
             if (b.zrl) {  // ZRL records (F/0) before the non-zeros after 16+ zeros (rare)
                 const uint32_t nzr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? b.run >> 4 : 0u;
@@ -279,7 +296,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 cp += 128;
                 cnA = cp[0];
                 cnB = cp[64];
-                const Blk A = prep(cA, jb), B = prep(cB, jb + 1);
+                const Blk A = prep(cA, jb, std::false_type{}), B = prep(cB, jb + 1, std::false_type{});
                 uint32_t baseB;
                 if (!(A.zrl || B.zrl)) {
                     // lanes without a record store out of range (dropped); their counter adds
@@ -303,12 +320,12 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                         if (__builtin_amdgcn_inverse_ballot_w64(fB)) atomicMin(&L.key[B.w], kkB);
                     }
                     base = baseB + (uint32_t)__builtin_popcountll(B.em);
-                } else {
-                    baseB = base + emit(A, base);
-                    base = baseB + emit(B, baseB);
+                } else {  // (a ZRL block: both again from the stage, exactly)
+                    baseB = base + emit(cp[-128], jb, base);
+                    base = baseB + emit(cp[-64], jb + 1, baseB);
                 }
             }
-            if (jb < j1) base += emit(prep(cnA, jb), base);  // an odd last block
+            if (jb < j1) base += emit(cnA, jb, base);  // an odd last block
         }
         JPGE_ACC(2, tq);
         if (lane == 0) a.tcount[s] = base;
