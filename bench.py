@@ -494,7 +494,7 @@ def run_striped16k(args, rank, local, world, pg):
     dt = max_over_ranks(pg, time.perf_counter() - t0)
     if rank == 0:
         print(json.dumps({
-            "metric": "MPixels/s encode (16K 4:2:0 Q=90)",
+            "metric": f"MPixels/s encode (16K 4:2:0 Q={args.quality})",
             "value": round(W * H * args.steps / dt / 1e6, 1), "unit": "MPix/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
@@ -681,7 +681,7 @@ def run_batch1080(args, rank, local, world, pg):
         bad = int(sum_over_ranks(pg, float(bad)))
     if rank == 0:
         line = {
-            "metric": "MPixels/s encode (batch of 256 x 1920x1080 4:2:0 Q=90)",
+            "metric": f"MPixels/s encode (batch of {B} x 1920x1080 4:2:0 Q={args.quality})",
             "value": round(W * H * B * args.steps / dt_max / 1e6, 1), "unit": "MPix/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
@@ -976,7 +976,7 @@ def run_frames(args, rank, local, world, pg):
 
     if rank == 0:
         line = {
-            "metric": f"MPixels/s encode (4K {sub_name(args)} Q=90)",
+            "metric": f"MPixels/s encode ({'4K' if (W, H) == (W4K, H4K) else f'{W}x{H}'} {sub_name(args)} Q={args.quality})",
             "value": round(value, 1),
             "unit": "MPix/s",
             "n_gpus": world,

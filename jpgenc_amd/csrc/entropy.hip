@@ -29,23 +29,10 @@ namespace jpge {
 namespace {
 using namespace dev;
 
-#ifndef K3_GROUPS
-#define K3_GROUPS 2  // code kernel: 4-record groups per thread and round (one scan and barrier per round)
-#endif
-#ifndef K3_WPE
+constexpr int kK3Groups = 2;  // code kernel: 4-record groups per thread and round (one scan and barrier per round)
 // waves per SIMD: one group fits 64 VGPRs at 8 (+4% in the pipeline over 4); two groups
 // need 72 (7 waves): +0.7% over one group at 8 (2 pairs on one box; 6 waves: +0.3%)
-#define K3_WPE (K3_GROUPS > 1 ? 7 : 8)
-#endif
-#ifndef K3_ZERO128
-#define K3_ZERO128 1  // (the stage zeroed in 16-byte stores; with K2's: 185.8 vs 184.4 GPix/s over 3 pairs)
-#endif
-#ifndef K3_EMIT_MERGE
-#define K3_EMIT_MERGE 1  // a thread's 4 records written as one bit string (code kernel)
-#endif
-#ifndef K3_PACK_BRANCHY
-#define K3_PACK_BRANCHY 1  // (measured: the branch-free 64-bit form ran 6 us slower per 4K frame)
-#endif
+constexpr int kK3Wpe = kK3Groups > 1 ? 7 : 8;
 constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
@@ -114,7 +101,7 @@ __device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, ui
 __device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int tid);
 
 template <int kN>
-__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_WPE))) void entropy_code_kernel(
+__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3Wpe))) void entropy_code_kernel(
     FrameSet<EntropyArgs, kN> fs) {
     __shared__ K3Lds L;
     const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
@@ -127,12 +114,9 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
     for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = lds_tab_entry(a.tables[i], (uint32_t)i);
-#if K3_ZERO128
+    // (the stage zeroed in 16-byte stores; with K2's: 185.8 vs 184.4 GPix/s over 3 pairs)
     static_assert(kStageWords % 4 == 0, "the stage zeroes in 16-byte stores");
     for (int i = tid; i < kStageWords / 4; i += kK3Threads) reinterpret_cast<uint4*>(L.stage)[i] = make_uint4(0, 0, 0, 0);
-#else
-    for (int i = tid; i < kStageWords; i += kK3Threads) L.stage[i] = 0;
-#endif
     const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
     const int ntl = (int)wt.nt * kRecSub;  // the tiles' record sub-streams (kernels.hpp)
     if (tid < 64) {  // (wave 0: ntl <= kTcntSlots <= 64) the counts, and their padded prefix
@@ -175,7 +159,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
     constexpr uint32_t slot = kSubRecords;  // records per sub-stream
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * slot * 4, 0x00020000);
-    constexpr int kGroups = K3_GROUPS;            // groups of 4 records per thread and round
+    constexpr int kGroups = kK3Groups;            // groups of 4 records per thread and round
     constexpr uint32_t kRound = 4 * kGroups * kK3Threads;  // records per round
     // The workgroup's records are one stream over its tiles: tile t's count padded to a
     // multiple of 4 (so a thread's 4 records are in one tile; the padding is never
@@ -234,7 +218,6 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
         uint32_t bp = pos + ex;
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
-#if K3_EMIT_MERGE
         // A group's 4 records are adjacent in the stream: concatenated in a 64-bit word
         // they touch at most three stage words, of which only the first and the last
         // can be shared with a neighbour (LDS OR); a middle word is the thread's alone
@@ -256,13 +239,11 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
                 if (end > 64) atomicOr(&L.stage[w + 2], lo << (32 - sh));
             }
             bp += tg;
-        } else
-#endif
-        {
+        } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            // each record into the one or two stage words it spans
-#if K3_PACK_BRANCHY
+            // each record into the one or two stage words it spans (a branch per record:
+            // a branch-free 64-bit form ran 6 us slower per 4K frame)
             if (cl[g][q]) {
                 const uint32_t sh = bp & 31, n = cl[g][q];
                 const uint32_t v = cb[g][q] << (32 - n);  // MSB-aligned (n >= 1)
@@ -270,13 +251,6 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(K3_W
                 if (sh + n > 32) atomicOr(&L.stage[(bp >> 5) + 1], v << (32 - sh));
                 bp += n;
             }
-#else
-            const uint32_t n = cl[g][q], sh = bp & 31;
-            const uint64_t v = n ? ((uint64_t)cb[g][q] << (64 - n)) >> sh : 0ull;  // MSB-aligned at bp
-            atomicOr(&L.stage[bp >> 5], (uint32_t)(v >> 32));
-            if ((uint32_t)v) atomicOr(&L.stage[(bp >> 5) + 1], (uint32_t)v);
-            bp += n;
-#endif
         }
         }
         }
@@ -609,10 +583,7 @@ __device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int 
 // entropy_place_kernel — the scan kernel's place mode in a smaller workgroup for
 // grids up to kPlaceSmallMaxWgs (restart off): a 4-wave workgroup finds a CU beside
 // the other lanes' kernels sooner than a 16-wave one, and the lane's stream waits on it.
-#ifndef K3_PLACE_THREADS
-#define K3_PLACE_THREADS 256
-#endif
-constexpr int kPlaceThreads = K3_PLACE_THREADS;
+constexpr int kPlaceThreads = 256;
 constexpr uint32_t kPlaceSmallMaxWgs = 4096;
 __global__ __launch_bounds__(kPlaceThreads) void entropy_place_kernel(EntropyArgs a, uint32_t G) {
     __shared__ uint32_t wsum[2 * (kPlaceThreads / 64)];

@@ -79,29 +79,17 @@ __device__ __forceinline__ u32x4 quant_row(const double o[8], const double c[8],
 }
 
 constexpr uint32_t kOob = 0xFFFFFF00u;  // buffer offset past every descriptor's range
-#ifndef K1_STORE_AUX
-#define K1_STORE_AUX 16  // sc1: write-through coefficient stores (no dirty L2 lines at the kernel's end)
-#endif
-#ifndef K1_SHARED_CAP
-#define K1_SHARED_CAP 512  // shared-shape workgroups per launch, at most (2 per CU: measured
-                            // +1.5% in the pipeline over 1024, which filled every CU)
-#endif
-#ifndef K1_LOAD_AUX
-#define K1_LOAD_AUX 0
-#endif
+constexpr int kK1StoreAux = 16;  // sc1: write-through coefficient stores (no dirty L2 lines at the kernel's end)
+constexpr uint32_t kK1SharedCap = 512;  // shared-shape workgroups per launch, at most (2 per CU: measured
+                                        // +1.5% in the pipeline over 1024, which filled every CU)
 
 // Workgroup shapes: whole-CU, one 16-wave workgroup per CU (4 waves per SIMD), whose
 // waves balance their tiles among themselves — for large frames with the GPU to
 // itself (two 8-wave workgroups per CU: equal at 4K, 4% slower at 16384^2); 4 waves,
 // four per CU alone (smaller frames, launch_fdct) or at most two per CU beside other
 // lanes' kernels (a whole-CU workgroup waits for a whole CU to drain).
-#ifndef K1_WAVES_SOLO
-#define K1_WAVES_SOLO 16
-#endif
-#ifndef K1_WAVES_SHARED
-#define K1_WAVES_SHARED 4  // (pipeline: 8 waves x 256 -1.4%, 8 x 512 -3.3%, 2 x 1024 -2.3%)
-#endif
-constexpr int kK1WavesSolo = K1_WAVES_SOLO, kK1WavesShared = K1_WAVES_SHARED;
+constexpr int kK1WavesSolo = 16;
+constexpr int kK1WavesShared = 4;  // (pipeline: 8 waves x 256 -1.4%, 8 x 512 -3.3%, 2 x 1024 -2.3%)
 constexpr int kRgbPitch = 66;    // u32 per staged pixel row: Y column reads conflict-free
 constexpr int kTmpBlock = 72;    // doubles per transpose block (rows of 9 doubles)
 constexpr int kTmpRow = 9;
@@ -234,9 +222,9 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
         const bool ok = k < n_p && aligned && y < gh_ && xs + 16 <= gw_;
         const uint32_t base = (uint32_t)((uint64_t)(mrow * 16) * stride_ + (uint64_t)mcol0 * 48);  // (uniform)
         const uint32_t off = ok ? base + lane_off : kOob;
-        v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
-        v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
-        v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, K1_LOAD_AUX));
+        v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, 0));
+        v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, 0));
+        v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, 0));
         return ok;
     };
     // The last round's 16-byte coefficient row (kOob: none) is stored during the
@@ -244,7 +232,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
     // then finds only long-issued stores ahead of them in the in-order counter.
     u32x4 pend;
     uint32_t poff = kOob;
-    auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, K1_STORE_AUX); };
+    auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, kK1StoreAux); };
     uint32_t k = __builtin_amdgcn_readfirstlane((uint32_t)wv);  // this wave's current tile of the run
     uint4 c0, c1, c2;
     bool cfast = fast_load(k, c0, c1, c2);  // issued before the prologue's own memory traffic
@@ -442,7 +430,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
                 load_y(0, p);
                 load_iq(0, iq);
             });
-            __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, kK1StoreAux);
         }
         {
             double x[8];
@@ -450,7 +438,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_kernel(FrameSet<FdctArgs, kN
             u32x4 pk;
             uint32_t off;
             finish(x, b8 >> 2, b8 & 3, 0, pk, off, [&] { load_y(1, p); });
-            __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, kK1StoreAux);
         }
         {
             double x[8];
@@ -529,14 +517,14 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArg
         const bool ok = k < n_p && aligned && y < gh_ && xs + 16 <= gw_;
         const uint32_t base = (uint32_t)((uint64_t)(mrow * 8) * stride_ + (uint64_t)mcol0 * 24 * kYh);  // (uniform)
         const uint32_t off = ok ? base + lane_off : kOob;
-        v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, K1_LOAD_AUX));
-        v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, K1_LOAD_AUX));
-        v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, K1_LOAD_AUX));
+        v0 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off, 0, 0));
+        v1 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 16, 0, 0));
+        v2 = as_u4(__builtin_amdgcn_raw_buffer_load_b128(rgb_rs, off + 32, 0, 0));
         return ok;
     };
     u32x4 pend;
     uint32_t poff = kOob;
-    auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, K1_STORE_AUX); };
+    auto store_pending = [&] { __builtin_amdgcn_raw_buffer_store_b128(pend, coef_rs, poff, 0, kK1StoreAux); };
     uint32_t k = __builtin_amdgcn_readfirstlane((uint32_t)wv);
     uint4 c0, c1, c2;
     bool cfast = fast_load(k, c0, c1, c2);
@@ -653,7 +641,7 @@ __global__ __launch_bounds__(kWaves * 64) void fdct_row8_kernel(FrameSet<FdctArg
             const uint32_t blk = (mrow * mw + mcol0 + m) * kBpm + slot;
             const uint32_t off = m < nvalid ? blk * 128 + j * 16 : kOob;
             if (round < kRounds - 1) {
-                __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, K1_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(pk, coef_rs, off, 0, kK1StoreAux);
             } else {
                 pend = pk;
                 poff = off;
@@ -715,9 +703,9 @@ uint32_t fdct_grid(const Geometry& g, bool solo, uint32_t override_wgs) {
         return tiles < cap ? tiles : cap;
     }
     // the 4-wave shape, a tile per wave at a time: four per CU alone, at most
-    // K1_SHARED_CAP beside other lanes
+    // kK1SharedCap beside other lanes
     const uint32_t wgs = (tiles + kK1WavesShared - 1) / kK1WavesShared;
-    const uint32_t cap = override_wgs ? override_wgs : solo ? 1024u : (uint32_t)K1_SHARED_CAP;
+    const uint32_t cap = override_wgs ? override_wgs : solo ? 1024u : kK1SharedCap;
     return wgs < cap ? wgs : cap;
 }
 

@@ -46,16 +46,10 @@ struct Geometry {
 // component of MCU slot k: 0 = Y, 1 = Cb, 2 = Cr (the last two slots are the chroma)
 JPGE_HD inline int block_comp(int k, uint32_t bpm) { return k < (int)bpm - 2 ? 0 : k - ((int)bpm - 3); }
 
-#ifndef JPGE_HIST_REPLICAS
-#define JPGE_HIST_REPLICAS 8
-#endif
-constexpr int kHistReplicas = JPGE_HIST_REPLICAS;  // spread of the global histogram atomics
+constexpr int kHistReplicas = 8;  // spread of the global histogram atomics
 constexpr int kStatsTile = 128;           // blocks per statistics tile (4 lanes each)
 constexpr int kEntropyTile = 128;         // blocks per entropy tile (4 lanes each)
-#ifndef K3_MAX_TILES
-#define K3_MAX_TILES 4
-#endif
-constexpr int kEntropyMaxTilesPerWg = K3_MAX_TILES;  // tiles a persistent entropy workgroup may own
+constexpr int kEntropyMaxTilesPerWg = 4;  // tiles a persistent entropy workgroup may own
 constexpr int kStageBytesPerBlock = 216;  // >= worst-case 1665 bits of one block
 constexpr int kStampSlots = 16;           // diagnostic stamp words per workgroup (JPGE_STAMPS builds)
 constexpr int kEntropyRecordBytes = 48;   // per entropy workgroup: bits, edge bits, 0xFF counts
