@@ -47,6 +47,9 @@ def main():
         ev = {"timed": b["stages"], "solo": b.get("stages_solo"),
               "solo_single": b.get("stages_solo_single_frame")}[label] or {}
         for k, v in ev.items():
+            if v.get("avg_kernel_ms") is None:
+                print(f"   bench HIP events {k:18s}     none (no timed launch)")
+                continue
             print(f"   bench HIP events {k:18s} {v['avg_kernel_ms'] * 1e3:8.2f} us "
                   f"(entropy = code + pack launches)")
 
