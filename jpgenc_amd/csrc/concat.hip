@@ -11,8 +11,8 @@
 // destination words are 16 apart), so each thread does two 16-byte buffer loads and
 // four v_alignbyte under a workgroup-uniform switch.  The (at most two) destination
 // words a segment shares with its neighbours are written byte by byte: every byte has
-// exactly one writer.  Sources go through buffer descriptors bounded by the segment,
-// so the second load of a segment's last word reads zeros, never past the run.
+// exactly one writer.  Sources go through buffer descriptors bounded by the segment's
+// last aligned 16 bytes, so a load past them reads zeros, never another page.
 // HBM-bound: 2 bytes of traffic per byte copied.
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -44,9 +44,13 @@ __global__ __launch_bounds__(kConcatThreads) void concat_kernel(ConcatArgs a) {
     const uint32_t lead = (uint32_t)(d0 - wbase);     // bytes of word 0 before the segment
     const uint32_t sh = (s0 + 16u - lead) & 15u;       // the window's shift (uniform)
     const uint32_t dw = sh >> 2, b = sh & 3u;
+    // The descriptor ends at the 16-byte boundary after the run: a load holding a needed
+    // byte is then wholly in range (the range check drops whole dwords, so a bound at
+    // the run's last byte would zero the valid bytes of a straddling dword), and the
+    // <= 15 bytes read past the run share its last aligned 16 bytes (never another page).
     // (descriptor sizes are 32-bit: segments are far below 4 GB, launch_concat checks)
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sbase), 0, (int)(s0 + len), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(sbase), 0, (int)((s0 + len + 15) & ~(uint64_t)15), 0x00020000);
     const uint64_t w_lo = (uint64_t)chunk * kConcatWords;
     const uint64_t w_hi = w_lo + kConcatWords < nw ? w_lo + kConcatWords : nw;
     for (uint64_t w = w_lo + threadIdx.x; w < w_hi; w += kConcatThreads) {
