@@ -97,7 +97,8 @@ struct WaitGuess {
     double total_us = 0;
 };
 inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int nap_us = 0,
-                    const std::atomic<int>* queued = nullptr, WaitGuess* guess = nullptr) {
+                    const std::atomic<int>* queued = nullptr, WaitGuess* guess = nullptr,
+                    const std::function<bool()>* work = nullptr) {
     const bool nap = nap_us > 0;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
@@ -109,9 +110,15 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int 
         if (guess) ++guess->ready;
         return kOk;
     }
-    if (nap && guess && guess->frac > 0 && guess->first_sleep_us() > 3.0 * nap_us) {
-        std::this_thread::sleep_for(std::chrono::microseconds((long)guess->first_sleep_us()));
-        ++guess->naps;
+    // (idle work first: the first sleep only once there is none)
+    bool worked = false;
+    while (work && __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq && (*work)()) worked = true;
+    if (nap && guess && guess->frac > 0 && !worked) {
+        const double us = guess->first_sleep_us();
+        if (us > 3.0 * nap_us) {
+            std::this_thread::sleep_for(std::chrono::microseconds((long)us));
+            ++guess->naps;
+        }
     }
     for (uint32_t spins = 0;; ++spins) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) {
@@ -122,6 +129,7 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int 
             }
             return kOk;
         }
+        if (work && (*work)()) continue;
         if (nap) {
             std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
             if (guess) ++guess->naps;
@@ -461,7 +469,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->set_ = env_int("JPGE_SET", 0, 0, kMaxSet);
     e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
-    e->inline_tables_ = env_int("JPGE_INLINE_TABLES", 2, 0, 2);
+    e->inline_tables_ = env_int("JPGE_INLINE_TABLES", e->inline_tables_, 0, 3);
     e->nap_us_ = env_int("JPGE_NAP_US", e->nap_us_, 1, 1000);
     e->first_sleep_ = env_int("JPGE_FIRST_SLEEP", (int)(e->first_sleep_ * 100 + 0.5), 0, 95) / 100.0;
     // (the table pool sleeps first only when asked: the 1080p batch lost 9% to it)
@@ -936,14 +944,14 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
     return kOk;
 }
 
-int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait) {
+int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait, const std::function<bool()>* idle) {
     // (a first sleep only up to kFirstSleepMaxPixels: 16384^2 frames, few per lane and
     // irregular, lost 3.7% to it)
     // (a set's later members: their results follow the first one's within microseconds,
     // and their short waits would blur the estimate of the real one)
     WaitGuess* const guess =
         guess_wait && (uint64_t)s.g.width * s.g.height <= kFirstSleepMaxPixels ? s.guess_result : nullptr;
-    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, guess)) return w;
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, guess, idle)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[7]));
         std::lock_guard<std::mutex> g(times_mu_);
@@ -988,7 +996,9 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
     int st = phase1(s, f, qy, qc, flags, nullptr, true);
-    if (!st) st = build_tables(s, true);
+    // (serially: spawning threads for the four tables costs more than the ~14 us of a 4K
+    // frame's tables they would overlap)
+    if (!st) st = build_tables(s, false);
     if (!st) st = import_tables_copy(s);
     if (!st) st = launch_entropy_phase(s, nullptr);
     if (!st) st = finish(s, f, flags);
@@ -1003,7 +1013,8 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
-    if (inline_tables_ != 1 && !pool_ && n > 1) pool_.reset(new TablePool(table_threads_, pool_first_sleep_));
+    if ((inline_tables_ == 0 || inline_tables_ == 2) && !pool_ && n > 1)
+        pool_.reset(new TablePool(table_threads_, pool_first_sleep_));
     // Frames are dealt dynamically: a lane takes the batch's next frame (or frame set)
     // when its pipeline has room, so lanes finish together.  Lane 0 runs on the calling
     // thread.
@@ -1091,16 +1102,37 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
     // member m of the other for the carried duties.  The pipeline's edges fall back to a
     // standalone export kernel and a table copy.
     const int L = lookahead_, D = drain_lag_;
+    // (JPGE_INLINE_TABLES=3) this lane's frames whose tables are not built yet; the
+    // lane's waits build any whose histograms are in (the ~25 us of a 1080p frame's
+    // tables fill a wait instead of a pool worker's polling and hand-off)
+    std::vector<Slot*> pend;
+    pend.reserve((size_t)(L + D + 2) * set);
+    const std::function<bool()> build_ready = [&]() -> bool {
+        for (size_t q = 0; q < pend.size(); ++q) {
+            Slot& s = *pend[q];
+            if (s.tables_done.load(std::memory_order_relaxed)) {
+                pend.erase(pend.begin() + (long)q);
+                return true;
+            }
+            if (__atomic_load_n(&s.h_hist->seq, __ATOMIC_ACQUIRE) != s.seq) continue;
+            pend.erase(pend.begin() + (long)q);
+            s.tables_status = build_tables(s, false);
+            s.tables_done.store(1, std::memory_order_release);
+            return true;
+        }
+        return false;
+    };
     auto submit_tables = [&](Slot& s) {
         // Large frames: built by this lane's thread when the frame's entropy launch needs
         // them (below): no pool workers polling for histograms, no hand-off (4K: the same
         // throughput at 2.6 instead of 3.5 CPUs).  Small frames come several times as
         // often per lane; their tables go to the pool, whose workers build them beside
         // the lane threads (1080p batch: 90.2 vs 82.5 GPix/s).
-        s.inline_tables = inline_tables_ == 1 ||
+        s.inline_tables = inline_tables_ == 1 || inline_tables_ == 3 ||
                           (inline_tables_ == 2 && (uint64_t)s.g.width * s.g.height >= kInlineTablesMinPixels) || !pool_;
         if (s.inline_tables) {
             s.tables_done.store(0, std::memory_order_relaxed);
+            if (inline_tables_ == 3) pend.push_back(&s);
         } else if (pool_) {
             Slot* sp = &s;
             const int dev = device_;
@@ -1170,8 +1202,7 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
                 if (frame(j, m).status) continue;
                 Slot& s = slot(j, m);
                 if (s.inline_tables && !s.tables_done.load(std::memory_order_acquire)) {
-                    // (no pool: a single-frame encode builds its four tables in parallel)
-                    s.tables_status = build_tables(s, /*parallel=*/!pool_);
+                    s.tables_status = build_tables(s, /*parallel=*/false);
                     s.tables_done.store(1, std::memory_order_release);
                 }
                 while (!s.tables_done.load(std::memory_order_acquire)) {
@@ -1299,7 +1330,8 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         if (k >= 0 && k < n) {
             for (int m = 0; m < members(k); ++m) {
                 Slot& s = slot(k, m);
-                if (!frame(k, m).status) note(k, m, finish(s, frame(k, m), flags, /*guess_wait=*/m == 0));
+                if (!frame(k, m).status)
+                    note(k, m, finish(s, frame(k, m), flags, /*guess_wait=*/m == 0, pend.empty() ? nullptr : &build_ready));
                 else hipStreamSynchronize(s.stream);
             }
         }
@@ -1845,7 +1877,7 @@ int Encoder::encode_planes(const double* const planes[3], uint32_t rows, uint32_
     FrameDesc f;
     f.out = out;
     f.cap = cap;
-    int e = build_tables(s, true);
+    int e = build_tables(s, false);
     if (!e) e = import_tables_copy(s);
     if (!e) e = launch_entropy_phase(s, nullptr);
     if (!e) e = finish(s, f, flags);

@@ -8,6 +8,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <vector>
 
@@ -151,7 +152,8 @@ class Encoder {
     // phase 2b (GPU): table upload (when not carried) + entropy kernels
     int import_tables_copy(Slot& s);
     int launch_entropy_phase(Slot& s, Slot* exp);
-    int finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait = true);
+    // idle: work the wait may do between its polls (returns whether it did any)
+    int finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait = true, const std::function<bool()>* idle = nullptr);
     // one lane's software pipeline over the frames it takes from fr[0..total) through `next`
     // (frames go in sets of `set` when set > 1: a pipeline step is a set, one launch per kernel)
     int run_lane(Lane& ln, FrameDesc* fr, int total, std::atomic<int>* next, int set, const uint8_t qy[64],
@@ -184,8 +186,11 @@ class Encoder {
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int set_ = 0;               // JPGE_SET: frames per launch (0: batch_set_size decides)
     int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables (JPGE_INLINE_TABLES=0)
-    int inline_tables_ = 2;     // JPGE_INLINE_TABLES: 1 each lane's thread builds its frames' tables, 0 the
-                                // pool, 2 (default) by frame size (encoder.cpp kInlineTablesMinPixels)
+    // JPGE_INLINE_TABLES: who builds a frame's Huffman tables.  3 (default): its lane's
+    // thread, as soon as the histograms are in, inside the waits of its pipeline (or when
+    // the entropy launch needs them); 1: its lane's thread when the entropy launch needs
+    // them; 0: the table pool; 2: by frame size (encoder.cpp kInlineTablesMinPixels).
+    int inline_tables_ = 3;
     int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
     // JPGE_FIRST_SLEEP (percent): a lane's first sleep in a result wait, of its usual length
     // less twice its spread (WaitGuess).  At 80%: 4K host CPU 1.45 -> 1.22 at equal

@@ -441,22 +441,12 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         }
         return e;
     };
-    // Converged levels.  Once a level's packages weigh exactly what its input packages
-    // weighed (same count, same weights in the same order), the next level is fed the same
-    // weight sequence: the same leaves' heap and the same pushes, so the heap performs the
-    // same moves and pops the same slots.  Its pop order is the previous level's with each
-    // package replaced by its successor (node id + np), and it again produces the same
-    // weights, so every remaining level repeats it.  On 1080p frames 8-9 of the 15 levels.
-    bool converged = false;
     for (int lv = 0; lv < kLevels; ++lv) {
         const HeapItem* in = pk_[lv & 1] + 1;
         HeapItem* out = pk_[(lv + 1) & 1] + 1;
         const int m = n + np, npairs = m / 2;
         int e;
-        if (converged) {
-            for (int k = 0; k < m; ++k) srt[k] += (uint32_t)item_node(srt[k]) >= (uint32_t)n ? (HeapItem)np : 0;
-            e = -1;
-        } else if (!wrapped) {
+        if (!wrapped) {
             // levels[lv] = the leaves + levels[lv-1]'s packages, by weight, leaves first on
             // ties: a branch-free merge run from both ends at once (two independent chains)
             // (one loop body carries both chains: a chain step waits on its loads)
@@ -511,11 +501,6 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         }
         out[-1] = kLo;
         out[npairs] = kHi;
-        if (!converged && !wrapped && npairs == np) {
-            uint32_t diff = 0;
-            for (int k = 0; k < np; ++k) diff |= item_hi(out[k]) ^ item_hi(in[k]);
-            converged = diff == 0;
-        }
         np = npairs;
     }
     // levels[15]: levels[14]'s packages alone, pushed in non-decreasing weight, so its
