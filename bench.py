@@ -595,7 +595,7 @@ def run_batch1080(args, rank, local, world, pg):
     enc = J.Encoder(local, lanes=rank_lanes(args))
     gather, transport = None, None
     nsets = 1
-    if world > 1:
+    if world > 1 and not os.environ.get("JPGE_BENCH_NO_GATHER"):  # (diagnostic: encode only, no gather)
         import torch.distributed as dist
 
         from jpgenc_amd.gather import BatchGather
@@ -667,7 +667,7 @@ def run_batch1080(args, rank, local, world, pg):
     # verification: every frame of the last step, as rank 0 holds it, equals the
     # host-path encode of that frame (rank 0's own frames are in its output slots)
     bad = 0
-    if not args.no_verify:
+    if not args.no_verify and (world == 1 or gather is not None):
         if rank == 0:
             for i in range(B):
                 ref = enc.encode(host[i] if i in host else J.synth_rgb8(batch_seed(i), W, H), quality=args.quality)
