@@ -14,8 +14,10 @@ where its bytes go.  Two transports:
 The pack is one jpge_concat_segments launch (a HIP kernel, any byte alignment) on the
 caller's current stream; CPU tensors (the gloo tests) use torch.cat.  The frame
 lengths go to rank 0 alone, on a host-side gloo group (a few hundred bytes,
-posted without waiting): rank 0 needs them to size its receives and to find frames;
-the other ranks never wait for anyone's lengths.
+posted without waiting): rank 0 needs them to size its receives and to find frames.
+No rank waits for another within a batch: rank 0 completes a batch's length receives
+(and posts its p2p data receives) at the next post, so it starts its next encode
+while the slowest rank is still finishing this one.
 
 `post()` returns once the transfers are queued (nothing on the host waits for the GPU):
 the next batch's encode runs while they move.  The caller encodes into two sets of
@@ -58,6 +60,7 @@ class BatchGather:
         if self.cuda and self.dev_index is None:
             self.dev_index = torch.cuda.current_device()
         self.lens_wait_s = 0.0     # rank 0: host time spent waiting for the other ranks' lengths
+        self.lens_recv = [[], []]  # rank 0: the posted length receives of the batch in each buffer
         self.lens_out = [torch.zeros(self.nmax, dtype=torch.int64) for _ in range(2)]
         self.lens_all = [[torch.zeros(self.nmax, dtype=torch.int64) for _ in range(world)] for _ in range(2)]
         # rank 0: the batch, rank r's run at r * cap_bytes
@@ -150,34 +153,51 @@ class BatchGather:
             self.cat_ev[b] = ev
         self.last = b
         if self.rank == 0:
+            # this batch's lengths: receives posted now, completed at the next post (or
+            # wait()), so rank 0 starts its next encode without waiting for the slowest
+            # rank to finish this one; the previous batch's are completed first
+            self._complete(b ^ 1)
             got = self.lens_all[b]
-            waits = [dist.irecv(got[r], dist.get_global_rank(self.meta, r), group=self.meta)
-                     for r in range(1, self.world)]
-            t0 = time.perf_counter()
-            for w in waits:
-                w.wait()
-            self.lens_wait_s += time.perf_counter() - t0
             got[0].zero_()
             if lens:
                 got[0][:len(lens)] = torch.tensor(lens, dtype=torch.int64)
-            ops = []
-            if self.transport == "p2p":
-                for r in range(1, self.world):
-                    tot = int(got[r].sum())
-                    if tot:
-                        ops.append(dist.P2POp(dist.irecv, self.batch[b][r * self.cap:r * self.cap + tot],
-                                              dist.get_global_rank(self.group, r), group=self.group))
+            self.lens_recv[b] = [dist.irecv(got[r], dist.get_global_rank(self.meta, r), group=self.meta)
+                                 for r in range(1, self.world)]
             self.got[b] = got
             self.where[b] = None
-        else:
-            ops = [dist.P2POp(dist.isend, run, dist.get_global_rank(self.group, 0), group=self.group)] \
-                if total and self.transport == "p2p" else []
+        elif total and self.transport == "p2p":
+            self.pending[b] += dist.batch_isend_irecv(
+                [dist.P2POp(dist.isend, run, dist.get_global_rank(self.group, 0), group=self.group)])
+
+    def _complete(self, b: int) -> None:
+        """Rank 0: the length receives of the batch in buffer b, then (p2p) the receives of
+        its runs, each exactly its size at its region."""
+        waits = self.lens_recv[b]
+        if not waits:
+            return
+        self.lens_recv[b] = []
+        t0 = time.perf_counter()
+        for w in waits:
+            w.wait()
+        self.lens_wait_s += time.perf_counter() - t0
+        if self.transport != "p2p":
+            return
+        dist = self.dist
+        ops = []
+        for r in range(1, self.world):
+            tot = int(self.got[b][r].sum())
+            if tot:
+                ops.append(dist.P2POp(dist.irecv, self.batch[b][r * self.cap:r * self.cap + tot],
+                                      dist.get_global_rank(self.group, r), group=self.group))
         if ops:
             self.pending[b] += dist.batch_isend_irecv(ops)
 
     def wait(self) -> None:
         """Every posted transfer complete (rank 0: `batch` holds the last batch once every
         rank has returned from wait(), e.g. after a barrier)."""
+        for b in (self.last ^ 1, self.last):  # (the older batch's receives first, as they were posted)
+            if self.rank == 0:
+                self._complete(b)
         for b in (0, 1):
             for w in self.pending[b]:
                 w.wait()
