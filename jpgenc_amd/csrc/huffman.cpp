@@ -172,25 +172,60 @@ class HashOrder {
         }();
         return ok;
     }
+    // key % bucket count for byte keys, per distinct bucket count of buckets() (the
+    // modulo was most of order()'s time: a 64-bit division per key and rehash)
+    struct ModTable {
+        uint32_t nb[kMaxSyms + 1];  // the distinct counts, in growth order
+        int cnt = 0;
+        uint16_t mod[16][256];
+    };
+    static const ModTable& mods() {
+        static const ModTable t = [] {
+            ModTable m;
+            const uint32_t* bc = buckets();
+            for (int k = 0; k <= kMaxSyms && m.cnt < 16; ++k) {
+                if (m.cnt && m.nb[m.cnt - 1] == bc[k]) continue;
+                m.nb[m.cnt] = bc[k];
+                for (uint32_t x = 0; x < 256; ++x) m.mod[m.cnt][x] = (uint16_t)(x % bc[k]);
+                ++m.cnt;
+            }
+            return m;
+        }();
+        return t;
+    }
     // iteration order (indices into keys) after inserting distinct keys[0..n) (std::hash<int>:
     // the value as size_t, so a negative key hashes to 2^64 + key)
     static void order(const int* keys, int n, int* out) {
+        bool bytes = true;
+        for (int i = 0; i < n; ++i) bytes &= (uint32_t)keys[i] < 256u;
+        const ModTable& mt = mods();
+        if (bytes && mt.cnt < 16) order_with(keys, n, out, [&mt](int key, int gen) -> uint32_t {
+            return mt.mod[gen][key];
+        });
+        else order_with(keys, n, out, [&mt](int key, int gen) -> uint32_t {
+            return (uint32_t)(static_cast<size_t>(key) % mt.nb[gen]);
+        });
+    }
+    template <class Mod>
+    static void order_with(const int* keys, int n, int* out, Mod&& mod) {
         constexpr int kNone = -1, kBefore = -2;  // bucket empty / its predecessor is before_begin
         const uint32_t* bc = buckets();
         int next[kMaxSyms];
         int bucket[kMaxBuckets];  // node before the bucket's first node (usable())
         uint32_t nb = bc[0];
+        int gen = 0;  // nb = mods().nb[gen]
         int head = kNone;
         for (uint32_t b = 0; b < nb; ++b) bucket[b] = kNone;
         for (int i = 0; i < n; ++i) {
             if (bc[i + 1] != nb) {  // _M_rehash_aux (unique keys)
                 nb = bc[i + 1];
+                ++gen;
                 for (uint32_t b = 0; b < nb; ++b) bucket[b] = kNone;
                 int p = head, bbegin = 0;
                 head = kNone;
                 while (p != kNone) {
                     const int nx = next[p];
-                    const uint32_t b = (uint32_t)(static_cast<size_t>(keys[p]) % nb);
+                    const uint32_t b = mod(keys[p], gen);
                     if (bucket[b] == kNone) {
                         next[p] = head;
                         head = p;
@@ -207,7 +242,7 @@ class HashOrder {
                     p = nx;
                 }
             }
-            const uint32_t b = (uint32_t)(static_cast<size_t>(keys[i]) % nb);  // _M_insert_bucket_begin
+            const uint32_t b = mod(keys[i], gen);  // _M_insert_bucket_begin
             if (bucket[b] != kNone) {
                 if (bucket[b] == kBefore) {
                     next[i] = head;
@@ -219,7 +254,7 @@ class HashOrder {
             } else {
                 next[i] = head;
                 head = i;
-                if (next[i] != kNone) bucket[static_cast<size_t>(keys[next[i]]) % nb] = i;
+                if (next[i] != kNone) bucket[mod(keys[next[i]], gen)] = i;
                 bucket[b] = kBefore;
             }
         }
