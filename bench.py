@@ -243,14 +243,10 @@ def device_for(local: int) -> int:
 
 
 def rank_lanes(args) -> int:
-    """Encoder lanes of this rank: --lanes, else the library default (4), divided among
-    the ranks that share one GPU (--allow-shared-gpu): the GPU runs as many pipelines
-    as one rank would (beyond 4 concurrent pipelines every kernel slows more than the
-    overlap gains)."""
-    if args.lanes:
-        return args.lanes
-    per = args.devices.get("ranks_per_device", 1) if args.devices.get("shared") else 1
-    return 0 if per <= 1 else max(1, 4 // per)
+    """Encoder lanes of this rank: --lanes, else the library default (4), also when ranks
+    share a GPU (--allow-shared-gpu): 2 ranks x 4 lanes ran config 4 at 0.81x one rank on
+    the GPU, 2 x 2 lanes at 0.74x (profiles/r05_bench_batch1080_x2.json)."""
+    return args.lanes
 
 
 def gather_group(world: int):
