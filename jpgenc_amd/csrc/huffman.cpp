@@ -144,6 +144,30 @@ namespace {
 
 constexpr int kMaxSyms = 256;
 
+// LSD radix sort of a[0..n) by key(a[i]) (uint64_t, ascending, stable), one counting pass
+// per byte that differs among the keys (histogram keys and weights vary in 2-4 bytes).
+// Branch-free where std::sort mispredicts about every other comparison on a frame's
+// fresh data; n <= 2 * kMaxSyms.
+template <class T, class Key>
+void radix_sort(T* a, int n, Key key) {
+    if (n < 2) return;
+    T tmp[2 * kMaxSyms];
+    uint64_t diff = 0;
+    const uint64_t k0 = key(a[0]);
+    for (int i = 1; i < n; ++i) diff |= key(a[i]) ^ k0;
+    T* src = a;
+    T* dst = tmp;
+    for (int sh = 0; sh < 64; sh += 8) {
+        if (!((diff >> sh) & 0xFF)) continue;
+        uint32_t cnt[257] = {};
+        for (int i = 0; i < n; ++i) ++cnt[((key(src[i]) >> sh) & 0xFF) + 1];
+        for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
+        for (int i = 0; i < n; ++i) dst[cnt[(key(src[i]) >> sh) & 0xFF]++] = src[i];
+        std::swap(src, dst);
+    }
+    if (src != a) std::copy(src, src + n, a);
+}
+
 class HashOrder {
   public:
     // bucket_count() of a std::unordered_map<int, int> after k insertions (k <= kMaxSyms)
@@ -419,6 +443,8 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     // 1080p frame took 56 us in the library against 20 us linked statically).
     struct Work {
         HeapItem base[kMaxSyms], heap[2 * kCap + kHeapPad], srt_[2 * kCap + 3];
+        HeapItem rp_pop[2 * kCap];
+        uint32_t rp_w[kCap];
         HeapItem pk_[2][kCap + 2], lsrt_[kMaxSyms + 2];
         int kid_a[kMaxKids], kid_b[kMaxKids], mult[kMaxNodes], first[kMaxNodes];
     };
@@ -440,7 +466,7 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     HeapItem* const lsrt = lsrt_ + 1;  // the leaves by weight
     HeapItem* const srt = srt_ + 1;    // a level's pop order
     for (int i = 0; i < n; ++i) lsrt[i] = item(lcnt[i], i);
-    std::sort(lsrt, lsrt + n, [](HeapItem x, HeapItem y) { return item_hi(x) < item_hi(y); });
+    radix_sort(lsrt, n, [](HeapItem x) -> uint64_t { return item_hi(x); });
     lsrt[-1] = pk_[0][0] = kLo;
     lsrt[n] = pk_[0][1] = kHi;  // (levels[0]: no packages)
     int* const kid_a = W.kid_a;
@@ -448,6 +474,15 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     int* const mult = W.mult;
     int* const first = W.first;
     int nkids = 0, np = 0;
+    struct LightReplay {  // the last light replay's inputs and pops
+        bool valid = false;
+        uint32_t wl = 0, pbase = 0;
+        int e = -1, np = 0, nl = 0;
+        uint32_t* w;
+        HeapItem* pop;
+    } rp;
+    rp.w = W.rp_w;
+    rp.pop = W.rp_pop;
     // Weights are the reference's ints.  The merges need every weight strictly between the
     // sentinels; if a package's sum reaches 2^31 - 1 or wraps (counts near 2^31), the
     // later levels run the heap whole instead.
@@ -513,17 +548,38 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
             for (int k = 0; k <= e; ++k) srt[k] = heap_pop(heap, hn);
         } else if (e >= 0) {  // the same up to that tie, on its light items (heap_pop_light)
             const uint32_t wl = item_hi(srt[e]);  // (the tie ends at e: exactly srt[0..e] are light)
-            for (int k = 0; k < nbase; ++k) heap[k] = item_hi(base[k]) > wl ? kHi : base[k];
-            int hn = nbase;
-            for (int k = 0; k < np; ++k) {
-                if (item_hi(in[k]) > wl) {  // (the packages come in weight order: the rest are heavy)
-                    std::fill(heap + hn, heap + hn + (np - k), kHi);
-                    hn += np - k;
-                    break;
+            int nl = 0;  // the light packages (they come in weight order)
+            while (nl < np && item_hi(in[nl]) <= wl) ++nl;
+            // The light replay depends only on the threshold, the light packages' weights
+            // and the heap's size (the leaves are the same every level, the heavy items
+            // markers): when those equal the previous replay's, so do the pops, slot for
+            // slot, with each package replaced by its counterpart of this level (on 1080p
+            // frames the light items repeat on about half the levels).
+            bool same = rp.valid && wl == rp.wl && e == rp.e && np == rp.np && nl == rp.nl;
+            for (int k = 0; same && k < nl; ++k) same = item_hi(in[k]) == rp.w[k];
+            const uint32_t pbase = np ? (uint32_t)item_node(in[0]) : 0u;  // (packages are numbered in order)
+            if (same) {
+                const uint32_t shift = pbase - rp.pbase;
+                for (int k = 0; k <= e; ++k) {
+                    const HeapItem x = rp.pop[k];
+                    srt[k] = x + ((uint32_t)item_node(x) >= (uint32_t)n ? (HeapItem)shift : 0);
                 }
-                heap_push(heap, hn, in[k]);
+            } else {
+                for (int k = 0; k < nbase; ++k) heap[k] = item_hi(base[k]) > wl ? kHi : base[k];
+                int hn = nbase;
+                for (int k = 0; k < nl; ++k) heap_push(heap, hn, in[k]);
+                std::fill(heap + hn, heap + nbase + np, kHi);
+                hn = nbase + np;
+                for (int k = 0; k <= e; ++k) srt[k] = heap_pop_light(heap, hn, kHi);
+                rp.valid = true;
+                rp.wl = wl;
+                rp.e = e;
+                rp.np = np;
+                rp.nl = nl;
+                for (int k = 0; k < nl; ++k) rp.w[k] = item_hi(in[k]);
             }
-            for (int k = 0; k <= e; ++k) srt[k] = heap_pop_light(heap, hn, kHi);
+            std::copy(srt, srt + e + 1, rp.pop);
+            rp.pbase = pbase;
         }
         for (int k = 0; k < npairs; ++k) {
             const HeapItem a = srt[2 * k], b = srt[2 * k + 1];
@@ -575,8 +631,8 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
     // code_lengths (an unordered_map) receives symbols by (first package, symbol)
     int ins[kMaxSyms];
     for (int i = 0; i < n; ++i) ins[i] = i;
-    std::sort(ins, ins + n, [&](int x, int y) {
-        return first[x] != first[y] ? first[x] < first[y] : lsym[x] < lsym[y];
+    radix_sort(ins, n, [&](int x) -> uint64_t {
+        return ((uint64_t)(uint32_t)first[x] << 32) | ((uint32_t)lsym[x] ^ 0x80000000u);  // (signed symbols)
     });
     int ksym[kMaxSyms];
     for (int i = 0; i < n; ++i) ksym[i] = lsym[ins[i]];
@@ -669,7 +725,7 @@ bool build_table(const uint32_t counts[256], const uint64_t first_key[256], Huff
             ++n;
         }
     if (!n) return false;
-    std::sort(key, key + n);
+    radix_sort(key, n, [](uint64_t k) { return k; });
     for (int i = 0; i < n; ++i) {
         syms[i] = (int)(key[i] & 0xFF);
         cnts[i] = (int)counts[syms[i]];
