@@ -151,6 +151,19 @@ constexpr int kMaxSyms = 256;
 template <class T, class Key>
 void radix_sort(T* a, int n, Key key) {
     if (n < 2) return;
+    if (n <= 24) {  // (a DC table's ~10 symbols: insertion sort, cheaper than 256-bucket passes)
+        for (int i = 1; i < n; ++i) {
+            const T v = a[i];
+            const uint64_t kv = key(v);
+            int j = i - 1;
+            while (j >= 0 && key(a[j]) > kv) {
+                a[j + 1] = a[j];
+                --j;
+            }
+            a[j + 1] = v;
+        }
+        return;
+    }
     T tmp[2 * kMaxSyms];
     uint64_t diff = 0;
     const uint64_t k0 = key(a[0]);
@@ -511,85 +524,147 @@ void code_lengths_fast(const int* syms, const int* cnts, int n, int by_len[18][k
         }
         return e;
     };
+    // One level, merged: levels[lv] = the leaves + levels[lv-1]'s packages by weight,
+    // leaves first on ties, as two branch-free chains run from both ends at once (a chain
+    // step waits on its loads, so two in flight halve the wait).  The chains also pair
+    // consecutive items into this level's packages and mark ties (eq bit k: item k
+    // weighs as item k-1), which then give the last tie the heap decides (last_tie's rule
+    // on 64 positions at a time).  A heap replay up to that tie changes only which equal
+    // weights stand where, so the packages' weights stay and only their children are
+    // taken again.
+    constexpr int kEqWords = (2 * kCap + 64) / 64 + 1;
+    constexpr uint64_t kEven = 0x5555555555555555ull;  // (bit k: k even)
+    auto merge_level = [&](const HeapItem* in, HeapItem* out, int m, int npairs, bool& wrap) {
+        const int half = (m + 1) / 2, nk = nkids;
+        uint64_t E[kEqWords];
+        const int words = (m >> 6) + 1;  // (positions 0..m)
+        for (int w = 0; w < words; ++w) E[w] = 0;
+        int i = 0, j = 0, i2 = n - 1, j2 = np - 1;
+        HeapItem pf = kLo, pb = kHi;  // the front chain's previous item (k - 1), the back chain's (p + 1)
+        uint64_t accf = 0, accb = 0;
+        bool wr = false;
+        auto pair = [&](int q, HeapItem a, HeapItem b) {
+            kid_a[nk + q] = item_node(a);
+            kid_b[nk + q] = item_node(b);
+            const int64_t sum = (int64_t)item_w(a) + item_w(b);
+            wr |= sum >= INT32_MAX || sum <= INT32_MIN + 1;
+            out[q] = item((int32_t)(uint32_t)sum, n + nk + q);
+        };
+        for (int k = 0; k < half; ++k) {
+            const int p = m - 1 - k;
+            // from the end (an odd m's middle item is written by both chains)
+            const HeapItem a2 = lsrt[i2], b2 = in[j2];
+            const bool t2 = item_hi(b2) >= item_hi(a2);
+            const HeapItem cb = t2 ? b2 : a2;
+            srt[p] = cb;
+            j2 -= t2;
+            i2 -= !t2;
+            accb |= (uint64_t)(item_hi(pb) == item_hi(cb)) << ((p + 1) & 63);  // eq[p + 1]
+            if (((p + 1) & 63) == 0) {
+                E[(p + 1) >> 6] |= accb;
+                accb = 0;
+            }
+            if (!(p & 1) && (p >> 1) < npairs) pair(p >> 1, cb, pb);
+            pb = cb;
+            // from the front
+            const HeapItem a = lsrt[i], b = in[j];
+            const bool t = item_hi(b) < item_hi(a);
+            const HeapItem cf = t ? b : a;
+            srt[k] = cf;
+            j += t;
+            i += !t;
+            accf |= (uint64_t)(item_hi(cf) == item_hi(pf)) << (k & 63);  // eq[k]
+            if ((k & 63) == 63) {
+                E[k >> 6] |= accf;
+                accf = 0;
+            }
+            if (k & 1) pair(k >> 1, pf, cf);
+            pf = cf;
+        }
+        E[(half - 1) >> 6] |= accf;
+        E[(m - half + 1) >> 6] |= accb;
+        if (!(m & 1) && m >= 2) {  // (the middle tie of an even m: between the chains)
+            const int c = m / 2;
+            E[c >> 6] |= (uint64_t)(item_hi(srt[c]) == item_hi(srt[c - 1])) << (c & 63);
+        }
+        for (int q = half >> 1; q < ((m - half + 1) >> 1) && q < npairs; ++q) pair(q, srt[2 * q], srt[2 * q + 1]);
+        srt[-1] = kLo;
+        srt[m] = kHi;
+        wrap |= wr;
+        // the last harmful tie: eq[k] and (k even, eq[k-1], eq[k+1] or k past the pairs)
+        const int pe = m - (m & 1);
+        for (int w = words - 1; w >= 0; --w) {
+            const uint64_t prv = (E[w] << 1) | (w ? E[w - 1] >> 63 : 0ull);
+            const uint64_t nxt = (E[w] >> 1) | (w + 1 < words ? E[w + 1] << 63 : 0ull);
+            const int b0 = 64 * w;
+            const uint64_t ge = pe <= b0 ? ~0ull : pe >= b0 + 64 ? 0ull : ~0ull << (pe - b0);
+            const uint64_t H = E[w] & (kEven | prv | nxt | ge);
+            if (H) return b0 + 63 - __builtin_clzll(H);
+        }
+        return -1;
+    };
     for (int lv = 0; lv < kLevels; ++lv) {
         const HeapItem* in = pk_[lv & 1] + 1;
         HeapItem* out = pk_[(lv + 1) & 1] + 1;
         const int m = n + np, npairs = m / 2;
-        int e;
-        if (!wrapped) {
-            // levels[lv] = the leaves + levels[lv-1]'s packages, by weight, leaves first on
-            // ties: a branch-free merge run from both ends at once (two independent chains)
-            // (one loop body carries both chains: a chain step waits on its loads)
-            const int half = (m + 1) / 2;
-            int i = 0, j = 0, i2 = n - 1, j2 = np - 1;
-            for (int k = 0; k < half; ++k) {
-                // from the end (an odd m's extra step reads sentinels or unused items
-                // and its slot is rewritten by the front step below)
-                const HeapItem a2 = lsrt[i2], b2 = in[j2];
-                const bool t2 = item_hi(b2) >= item_hi(a2);
-                srt[m - 1 - k] = t2 ? b2 : a2;
-                j2 -= t2;
-                i2 -= !t2;
-                const HeapItem a = lsrt[i], b = in[j];
-                const bool t = item_hi(b) < item_hi(a);
-                srt[k] = t ? b : a;
-                j += t;
-                i += !t;
-            }
-            srt[-1] = kLo;
-            e = last_tie(m, m - (m & 1));
-        } else {
-            e = 2 * npairs - 1;
-        }
-        if (e >= 0 && wrapped) {  // the reference's heap: the leaves' heap, then the pushes
+        bool wrap_next = false;
+        if (wrapped) {  // the reference's heap: the leaves' heap, then the pushes, every pop
+            const int e = 2 * npairs - 1;
             int hn = nbase;
             std::copy(base, base + nbase, heap);
             for (int k = 0; k < np; ++k) heap_push(heap, hn, in[k]);
             for (int k = 0; k <= e; ++k) srt[k] = heap_pop(heap, hn);
-        } else if (e >= 0) {  // the same up to that tie, on its light items (heap_pop_light)
-            const uint32_t wl = item_hi(srt[e]);  // (the tie ends at e: exactly srt[0..e] are light)
-            int nl = 0;  // the light packages (they come in weight order)
-            while (nl < np && item_hi(in[nl]) <= wl) ++nl;
-            // The light replay depends only on the threshold, the light packages' weights
-            // and the heap's size (the leaves are the same every level, the heavy items
-            // markers): when those equal the previous replay's, so do the pops, slot for
-            // slot, with each package replaced by its counterpart of this level (on 1080p
-            // frames the light items repeat on about half the levels).
-            bool same = rp.valid && wl == rp.wl && e == rp.e && np == rp.np && nl == rp.nl;
-            for (int k = 0; same && k < nl; ++k) same = item_hi(in[k]) == rp.w[k];
-            const uint32_t pbase = np ? (uint32_t)item_node(in[0]) : 0u;  // (packages are numbered in order)
-            if (same) {
-                const uint32_t shift = pbase - rp.pbase;
-                for (int k = 0; k <= e; ++k) {
-                    const HeapItem x = rp.pop[k];
-                    srt[k] = x + ((uint32_t)item_node(x) >= (uint32_t)n ? (HeapItem)shift : 0);
-                }
-            } else {
-                for (int k = 0; k < nbase; ++k) heap[k] = item_hi(base[k]) > wl ? kHi : base[k];
-                int hn = nbase;
-                for (int k = 0; k < nl; ++k) heap_push(heap, hn, in[k]);
-                std::fill(heap + hn, heap + nbase + np, kHi);
-                hn = nbase + np;
-                for (int k = 0; k <= e; ++k) srt[k] = heap_pop_light(heap, hn, kHi);
-                rp.valid = true;
-                rp.wl = wl;
-                rp.e = e;
-                rp.np = np;
-                rp.nl = nl;
-                for (int k = 0; k < nl; ++k) rp.w[k] = item_hi(in[k]);
+            for (int k = 0; k < npairs; ++k) {
+                const HeapItem a = srt[2 * k], b = srt[2 * k + 1];
+                kid_a[nkids + k] = item_node(a);
+                kid_b[nkids + k] = item_node(b);
+                out[k] = item((int32_t)((uint32_t)item_w(a) + (uint32_t)item_w(b)), n + nkids + k);
             }
-            std::copy(srt, srt + e + 1, rp.pop);
-            rp.pbase = pbase;
+        } else {
+            const int e = merge_level(in, out, m, npairs, wrap_next);
+            if (e >= 0) {  // the heap up to that tie, on its light items (heap_pop_light)
+                const uint32_t wl = item_hi(srt[e]);  // (the tie ends at e: exactly srt[0..e] are light)
+                int nl = 0;  // the light packages (they come in weight order)
+                while (nl < np && item_hi(in[nl]) <= wl) ++nl;
+                // The light replay depends only on the threshold, the light packages'
+                // weights and the heap's size (the leaves are the same every level, the
+                // heavy items markers): when those equal the previous replay's, so do the
+                // pops, slot for slot, with each package replaced by its counterpart of
+                // this level (on 1080p frames the light items repeat on about half the
+                // levels).
+                bool same = rp.valid && wl == rp.wl && e == rp.e && np == rp.np && nl == rp.nl;
+                for (int k = 0; same && k < nl; ++k) same = item_hi(in[k]) == rp.w[k];
+                const uint32_t pbase = np ? (uint32_t)item_node(in[0]) : 0u;  // (packages are numbered in order)
+                if (same) {
+                    const uint32_t shift = pbase - rp.pbase;
+                    for (int k = 0; k <= e; ++k) {
+                        const HeapItem x = rp.pop[k];
+                        srt[k] = x + ((uint32_t)item_node(x) >= (uint32_t)n ? (HeapItem)shift : 0);
+                    }
+                } else {
+                    for (int k = 0; k < nbase; ++k) heap[k] = item_hi(base[k]) > wl ? kHi : base[k];
+                    int hn = nbase;
+                    for (int k = 0; k < nl; ++k) heap_push(heap, hn, in[k]);
+                    std::fill(heap + hn, heap + nbase + np, kHi);
+                    hn = nbase + np;
+                    for (int k = 0; k <= e; ++k) srt[k] = heap_pop_light(heap, hn, kHi);
+                    rp.valid = true;
+                    rp.wl = wl;
+                    rp.e = e;
+                    rp.np = np;
+                    rp.nl = nl;
+                    for (int k = 0; k < nl; ++k) rp.w[k] = item_hi(in[k]);
+                }
+                std::copy(srt, srt + e + 1, rp.pop);
+                rp.pbase = pbase;
+                for (int q = 0; q <= (e >> 1) && q < npairs; ++q) {  // (the replayed pairs' children)
+                    kid_a[nkids + q] = item_node(srt[2 * q]);
+                    kid_b[nkids + q] = item_node(srt[2 * q + 1]);
+                }
+            }
         }
-        for (int k = 0; k < npairs; ++k) {
-            const HeapItem a = srt[2 * k], b = srt[2 * k + 1];
-            kid_a[nkids] = item_node(a);
-            kid_b[nkids] = item_node(b);
-            const int64_t sum = (int64_t)item_w(a) + item_w(b);
-            wrapped |= sum >= INT32_MAX || sum <= INT32_MIN + 1;
-            out[k] = item((int32_t)(uint32_t)sum, n + nkids);
-            ++nkids;
-        }
+        nkids += npairs;
+        wrapped |= wrap_next;
         out[-1] = kLo;
         out[npairs] = kHi;
         np = npairs;
