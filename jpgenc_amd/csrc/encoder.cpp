@@ -200,6 +200,8 @@ struct CtlLayout {
     }
 };
 
+constexpr size_t kStatsDoneOff = 64;  // K2's finished-workgroup count: a line of its own in the `done` block
+
 struct HostHist {  // written by hist_export_kernel into mapped pinned memory
     uint32_t cnt[4 * 256];  // replicas summed
     uint64_t key[4 * 256];  // ~first-occurrence key
@@ -465,6 +467,8 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
     e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
+    e->lat_prof_ = env_int("JPGE_LAT_PROF", 0, 0, 1) != 0;
+    e->hist_nap_us_ = env_int("JPGE_HIST_NAP_US", e->hist_nap_us_, 0, 1000);
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->set_ = env_int("JPGE_SET", 0, 0, kMaxSet);
@@ -549,6 +553,12 @@ int Encoder::add_slots(Lane& ln, int count) {
 }
 
 Encoder::~Encoder() {
+    if (lat_prof_ && lat_calls_)
+        std::fprintf(stderr, "jpge encode() phases per call (us, wall): launch-1 %.2f histogram-wait %.2f tables %.2f "
+                             "launch-entropy %.2f result-wait %.2f end %.2f (%lld calls)\n",
+                     lat_ns_[0] / 1e3 / lat_calls_, lat_ns_[1] / 1e3 / lat_calls_, lat_ns_[2] / 1e3 / lat_calls_,
+                     lat_ns_[3] / 1e3 / lat_calls_, lat_ns_[4] / 1e3 / lat_calls_, lat_ns_[5] / 1e3 / lat_calls_,
+                     (long long)lat_calls_);
     if (cpu_prof_ && cpu_frames_.load()) {
         const double f = (double)cpu_frames_.load();
         std::fprintf(stderr, "jpge cpu per frame (us): tables %.2f launch-1 %.2f launch-entropy %.2f finish %.2f "
@@ -800,16 +810,18 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
     s.count_symbols = s.timed;
     // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
     const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
-    JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
-    JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2 : nullptr));
     s.seq = ++seq_counter_;
     s.hist = st2.hist;
-    if (export_hist)
-    {
-        JPGE_HIP(launch_hist_export(st2.hist, s.d_hist_host->cnt, s.d_hist_host->key, &s.d_hist_host->seq, s.seq,
-                                    s.stream));
-        s.export_queued.store(1, std::memory_order_release);
+    if (export_hist) {  // (by K2's last workgroup: no launch of its own)
+        st2.done = reinterpret_cast<uint32_t*>(s.d_ctl + CtlLayout(slot_layout(s).grid()).done + kStatsDoneOff);
+        st2.host_cnt = s.d_hist_host->cnt;
+        st2.host_key = s.d_hist_host->key;
+        st2.host_seq = &s.d_hist_host->seq;
+        st2.seq = s.seq;
     }
+    JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
+    JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2 : nullptr));
+    if (export_hist) s.export_queued.store(1, std::memory_order_release);
     return kOk;
 }
 
@@ -848,9 +860,10 @@ int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a_in, const Stats
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel) {
-    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : 10), &s.export_queued,
+    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : hist_nap_us_), &s.export_queued,
                                s.inline_tables ? s.guess_hist : nullptr))
         return w;
+    if (lat_prof_) lat_hist_seen_ = std::chrono::steady_clock::now();
     auto thread_ns = [] {
         timespec t;
         clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
@@ -995,14 +1008,41 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     std::lock_guard<std::recursive_mutex> call_lock(call_mu_);
     JPGE_HIP(hipSetDevice(device_));
     Slot& s = *lanes_[0]->slots[0];
+    using clk = std::chrono::steady_clock;
+    clk::time_point T[6];
+    if (lat_prof_) T[0] = clk::now();
     int st = phase1(s, f, qy, qc, flags, nullptr, true);
+    if (lat_prof_) T[1] = clk::now();
     // (serially: spawning threads for the four tables costs more than the ~14 us of a 4K
     // frame's tables they would overlap)
     if (!st) st = build_tables(s, false);
+    if (lat_prof_) T[2] = clk::now();
     if (!st) st = import_tables_copy(s);
     if (!st) st = launch_entropy_phase(s, nullptr);
+    if (lat_prof_) T[3] = clk::now();
     if (!st) st = finish(s, f, flags);
-    hipStreamSynchronize(s.stream);  // every output byte is in place
+    if (lat_prof_) T[4] = clk::now();
+    // every output byte is in place: the stream's tail, awaited by spinning as a batch
+    // lane's end (a blocking stream synchronisation took ~9 us after the result word)
+    if (end_sync_ == 2 || hipEventRecord(lanes_[0]->done, s.stream) != hipSuccess) {
+        hipStreamSynchronize(s.stream);
+    } else {
+        const hipError_t w = end_sync_ == 1 ? hipEventSynchronize(lanes_[0]->done) : wait_event(lanes_[0]->done);
+        if (w != hipSuccess && !st) st = kErrHip;
+    }
+    if (lat_prof_ && !st) {
+        T[5] = clk::now();
+        auto ns = [](clk::time_point a, clk::time_point b) {
+            return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+        };
+        lat_ns_[0] += ns(T[0], T[1]);
+        lat_ns_[1] += ns(T[1], lat_hist_seen_);
+        lat_ns_[2] += ns(lat_hist_seen_, T[2]);
+        lat_ns_[3] += ns(T[2], T[3]);
+        lat_ns_[4] += ns(T[3], T[4]);
+        lat_ns_[5] += ns(T[4], T[5]);
+        ++lat_calls_;
+    }
     f.status = st;
     return st;
 }

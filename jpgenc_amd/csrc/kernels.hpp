@@ -171,6 +171,14 @@ struct StatsArgs {
     uint32_t* tcount;    // [tiles][kRecSub] records per sub-stream
     uint32_t wgs = 0;    // workgroup count (0 = 3 per CU; the pipeline passes its own, stats_grid)
     uint64_t* dbg;
+    // Set (single frames): the last workgroup to finish exports the histograms into
+    // mapped host memory (export_hist), in place of a hist_export_kernel launch.  `done`
+    // counts finished workgroups (zeroed per frame by K1).
+    uint32_t* done = nullptr;
+    uint32_t* host_cnt = nullptr;
+    uint64_t* host_key = nullptr;
+    uint64_t* host_seq = nullptr;
+    uint64_t seq = 0;
 };
 
 // Where each entropy workgroup's bytes go (entropy_scan_kernel -> pack kernel).

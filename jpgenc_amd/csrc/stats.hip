@@ -121,7 +121,24 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     }
     if (tid == 0) L.next = kWWaves;  // (sub-stream w is wave w's first)
     __syncthreads();
-    if (ns == 0) return;
+    // (single frames) the histogram export by the last workgroup to finish: every
+    // workgroup counts itself once its flush atomics (device-coherent) have completed;
+    // the one completing the count reads every workgroup's counts and keys
+    auto export_if_last = [&]() {
+        if (!a.done) return;
+        vm_drain();
+        __syncthreads();
+        if (tid == 0) L.next = atomicAdd(a.done, 1u) == nbk - 1 ? 1u : 0u;
+        __syncthreads();
+        if (L.next) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            export_hist<kWThreads>(a.hist, a.host_cnt, a.host_key, a.host_seq, a.seq, tid);
+        }
+    };
+    if (ns == 0) {
+        export_if_last();
+        return;
+    }
     // key bases (keys are kept relative to them): the workgroup's first MCU row
     const uint32_t mrow0 = __builtin_amdgcn_readfirstlane((L.sb0[0] / bpm) / mw);
     const uint32_t ybase = mrow0 * yv * ybw, cbase = mrow0 * mw;
@@ -356,6 +373,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[i]);
         if (inv > *gk) atomicMax(gk, inv);
     }
+    export_if_last();
     JPGE_STAMP(3);
 }
 
