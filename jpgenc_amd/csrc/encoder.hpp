@@ -192,7 +192,7 @@ class Encoder {
     // the entropy launch needs them); 1: its lane's thread when the entropy launch needs
     // them; 0: the table pool; 2: by frame size (encoder.cpp kInlineTablesMinPixels).
     int inline_tables_ = 3;
-    int nap_us_ = 10;           // JPGE_NAP_US: a napping thread's sleep between polls
+    int nap_us_ = 40;           // JPGE_NAP_US: a napping thread's sleep between polls (10: equal throughput, more wake-ups)
     // JPGE_FIRST_SLEEP (percent): a lane's first sleep in a result wait, of its usual length
     // less twice its spread (WaitGuess).  At 80%: 4K host CPU 1.45 -> 1.22 at equal
     // throughput; frames above kFirstSleepMaxPixels (16384^2: -3.7%) poll without it.
