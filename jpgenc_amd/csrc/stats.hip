@@ -195,10 +195,11 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         const uint32_t rel = comp == 0 ? (mrow * yv + (k >> yhs)) * ybw + mcol * yh + (k & (yh - 1)) - ybase
                                        : (m6 - cbase) | (comp == 2 ? 0x80000000u : 0u);
         const uint32_t tsel = comp != 0;
-        // the block loop reads two words per block: the AC key base (text index * 128 + 1;
-        // a key is base + 2p), and the AC table as a record's top byte | its first counter word
-        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7) | 1u;
-        const uint32_t tw = ((2u * tsel + 1u) << 24) | tab_base(2u * tsel + 1u);
+        // the block loop reads one word per block: the AC key base, text index * 128 + d,
+        // whose low bit d is the table select (a key is base + 2p: keys are compared only
+        // within a table, where d is constant; a ZRL's key base + 2p - 1 still sorts
+        // between positions p - 1 and p)
+        const uint32_t acb = (rel & 0x80000000u) | ((rel & 0x7FFFFFFFu) << 7) | tsel;
         // DC difference to the chain predecessor: the previous Y slot, 3 blocks back for an
         // MCU's first Y block, bpm back for chroma; none in the first MCU; restarts reset it
         int dd;
@@ -239,10 +240,10 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             Blk b;
             const uint64_t B1 = __ballot(c != 0) | 1ull;  // the AC non-zeros, and bit 0
             b.M = B1 & lanes_ac;
-            const uint32_t twj = __builtin_amdgcn_readlane(tw, jb);
-            b.Tj = twj & 0xFF000000u;                       // the AC table, as a record's top byte
-            b.acw = twj & 0xFFFFu;                          // its first counter / key word
-            b.acbj = __builtin_amdgcn_readlane(acb, jb);    // (+ 2p: the key; the EOB lane 63: text * 128 + 127)
+            b.acbj = __builtin_amdgcn_readlane(acb, jb);    // (+ 2p: the key; the EOB lane 63: text * 128 + 126 + d)
+            const uint32_t d = b.acbj & 1u;                  // (scalar: 1 for the chroma tables)
+            b.Tj = 0x01000000u + (d << 25);                  // the AC table, as a record's top byte
+            b.acw = d * tab_base(3);                         // its first counter / key word (tab_base(1) = 0)
             b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0u));
             if constexpr (kExact) b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
             else b.run = (uint32_t)__builtin_clz((uint32_t)((B1 << shl) >> 32) | 1u);
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             // codes the block's DC symbol like an AC lane: its record (its table: the AC
             // table's number less one; the run of 16 sets a bit the table byte has) at the
             // block's first record (rank 0), its count in the DC table's word (kDcOff past
-            // the AC table's first), its key as text index * 128 + 1 (the flush divides
+            // the AC table's first), its key as text index * 128 + d (the flush divides
             // it back).  Stored after the sub-stream, the DC records had rewritten lines
             // already written back (K2 wrote 1.24x its record bytes); counted after the
             // sub-stream, they cost a pass of their own.
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         uint64_t kb;  // (global texts: a stripe's bases are offset into the whole image)
         if (t < 2) kb = a.key_y0 + ybase;
         else kb = a.key_c0 + cbase + ((k32 & 0x80000000u) ? ncb : 0ull);
-        // (AC keys: text index * 128 + 2p + delta; DC keys were kept as text index * 128 + 1)
+        // (AC keys: text index * 128 + 2p + delta + d; DC keys were kept as text index * 128 + d)
         const uint64_t gkey = (t & 1) ? kb * 128ull + (k32 & 0x7FFFFFFFu) : kb + ((k32 & 0x7FFFFFFFu) >> 7);
         const unsigned long long inv = ~gkey;
         unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[i]);
