@@ -307,13 +307,9 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             if (j0 >= nb) continue;
             const uint32_t j1 = min(nb, j0 + 8u);
             const int16_t* cp = st16 + natoff;  // (the pair after the chunk's last reads past it: unused)
-            int cnA = cp[0], cnB = cp[64];
             uint32_t jb = j0;
-            for (; jb + 1 < j1; jb += 2) {
-                const int cA = cnA, cB = cnB;
-                cp += 128;
-                cnA = cp[0];
-                cnB = cp[64];
+            for (; jb + 1 < j1; jb += 2, cp += 128) {
+                const int cA = cp[0], cB = cp[64];
                 const Blk A = prep(cA, jb, std::false_type{}), B = prep(cB, jb + 1, std::false_type{});
                 uint32_t baseB;
                 if (!(A.zrl || B.zrl)) {
@@ -339,11 +335,11 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                     }
                     base = baseB + (uint32_t)__builtin_popcountll(B.em);
                 } else {  // (a ZRL block: both again from the stage, exactly)
-                    baseB = base + emit(cp[-128], jb, base);
-                    base = baseB + emit(cp[-64], jb + 1, baseB);
+                    baseB = base + emit(cp[0], jb, base);
+                    base = baseB + emit(cp[64], jb + 1, baseB);
                 }
             }
-            if (jb < j1) base += emit(cnA, jb, base);  // an odd last block
+            if (jb < j1) base += emit(cp[0], jb, base);  // an odd last block
         }
         JPGE_ACC(2, tq);
         if (lane == 0) a.tcount[s] = base;

@@ -1,31 +1,54 @@
 #!/bin/bash
-# Round profiles in one GPU call (run through gpurun), on the final tree:
-#   1. the bench line with the CPU baseline (default arguments)     -> gpurun_out/rp/bench.json
-#   2. rocprofv3 --kernel-trace --stats of a shorter bench run       -> gpurun_out/rp/trace/
-#      + per-kernel means in its timed / solo windows next to the bench's
-#        kernel-bound event averages                                  -> gpurun_out/rp/window.txt
-#   3. HBM traffic, two --pmc passes (FETCH_SIZE, WRITE_SIZE) of a small bench run,
-#      one frame per launch (JPGE_SET=1: per-frame bytes)          -> gpurun_out/pmc_rp.json
-#   4. SQ counters (2 passes) of the single-frame loop                -> gpurun_out/sq_rp/
-#   5. config 4 (batch1080) and 16384^2 bench lines                   -> gpurun_out/rp/{b1080,16k}.json
+# Round profiles on the final tree, in two GPU calls (run through gpurun):
+#   part A: the GPU test suite and smoke()                            -> gpurun_out/rp/{gpu_tests,smoke}.log
+#           the bench line with the CPU baseline (default arguments)  -> gpurun_out/rp/bench.json
+#           rocprofv3 --kernel-trace --stats of a shorter bench run   -> gpurun_out/rp/trace/
+#             + per-kernel means in its timed / solo windows next to the bench's
+#               kernel-bound event averages                           -> gpurun_out/rp/window.txt
+#           HBM traffic, two --pmc passes (FETCH_SIZE, WRITE_SIZE) of a small bench run,
+#             one frame per launch (JPGE_SET=1: per-frame bytes)      -> gpurun_out/pmc_rp.json
+#           SQ counters (2 passes) of the single-frame loop           -> gpurun_out/sq_rp/
+#   part B: config 3's quality sweep (Q50, Q100 bench lines)          -> gpurun_out/rp/q{50,100}.json
+#           config 4 (batch1080) on one rank and on 2 ranks sharing the GPU
+#                                                                     -> gpurun_out/rp/b1080{,x2}.json
+#           16384^2 frames through the pipeline                       -> gpurun_out/rp/16k.json
+#   tools/round_profiles.sh A|B
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" || exit 1
 export TMPDIR=/tmp
-mkdir -p gpurun_out/rp
-timeout -k 10 400 python3 bench.py > gpurun_out/rp/bench.json 2> gpurun_out/rp/bench.err || { tail -5 gpurun_out/rp/bench.err; exit 1; }
-tail -c 300 gpurun_out/rp/bench.json; echo
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp/trace -o run -- \
-  python3 bench.py --no-cpu-baseline --frames 768 --steps 10 > gpurun_out/rp/prof_bench.json 2> gpurun_out/rp/prof.err || { tail -5 gpurun_out/rp/prof.err; exit 1; }
-python3 tools/rocprof_window.py gpurun_out/rp/trace gpurun_out/rp/prof_bench.json | tee gpurun_out/rp/window.txt
-JPGE_SET=1 bash tools/pmc_traffic.sh rp --frames 64 --steps 2 --warmup 1 --solo-batches 0 --d2h-steps 0 --no-verify || exit 1
-python3 tools/pmc_summary.py gpurun_out/pmc_rp | tail -40
-bash tools/pmc_sq.sh rp --iters 8 > gpurun_out/rp/sq.txt 2>&1 || { tail -5 gpurun_out/rp/sq.txt; exit 1; }
-timeout -k 10 300 python3 bench.py --workload batch1080 > gpurun_out/rp/b1080.json 2> gpurun_out/rp/b1080.err || { tail -5 gpurun_out/rp/b1080.err; exit 1; }
-tail -c 300 gpurun_out/rp/b1080.json; echo
-timeout -k 10 300 python3 bench.py --width 16384 --height 16384 --frames 16 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/rp/16k.json 2> gpurun_out/rp/16k.err || { tail -5 gpurun_out/rp/16k.err; exit 1; }
-tail -c 300 gpurun_out/rp/16k.json; echo
-# keep the summaries (gpurun copies back <= 64 MiB): drop the per-dispatch CSVs
-find gpurun_out/rp/trace gpurun_out/pmc_rp gpurun_out/sq_rp -name '*kernel_trace.csv' -exec gzip -9 {} + 2>/dev/null
-find gpurun_out/pmc_rp gpurun_out/sq_rp -name '*counter_collection.csv' -exec gzip -9 {} + 2>/dev/null
+O=gpurun_out/rp
+mkdir -p $O
+line() { tail -c 400 "$1"; echo; }
+case "${1:-A}" in
+A)
+  timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+  tail -1 $O/gpu_tests.log
+  timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -10 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+  timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+  line $O/bench.json
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+    python3 bench.py --no-cpu-baseline --frames 768 --steps 10 --latency-calls 0 > $O/prof_bench.json 2> $O/prof.err || { tail -5 $O/prof.err; exit 1; }
+  python3 tools/rocprof_window.py $O/trace $O/prof_bench.json | tee $O/window.txt
+  JPGE_SET=1 bash tools/pmc_traffic.sh rp --frames 64 --steps 2 --warmup 1 --solo-batches 0 --d2h-steps 0 --latency-calls 0 --no-verify || exit 1
+  python3 tools/pmc_summary.py gpurun_out/pmc_rp | tail -40
+  bash tools/pmc_sq.sh rp --iters 8 > $O/sq.txt 2>&1 || { tail -5 $O/sq.txt; exit 1; }
+  # keep the summaries (gpurun copies back <= 64 MiB): drop the per-dispatch CSVs
+  find $O/trace gpurun_out/pmc_rp gpurun_out/sq_rp -name '*kernel_trace.csv' -exec gzip -9 {} + 2>/dev/null
+  find gpurun_out/pmc_rp gpurun_out/sq_rp -name '*counter_collection.csv' -exec gzip -9 {} + 2>/dev/null
+  ;;
+B)
+  for q in 50 100; do
+    timeout -k 10 400 python3 bench.py --quality $q --no-cpu-baseline > $O/q$q.json 2> $O/q$q.err || { tail -5 $O/q$q.err; exit 1; }
+    line $O/q$q.json
+  done
+  timeout -k 10 300 python3 bench.py --workload batch1080 > $O/b1080.json 2> $O/b1080.err || { tail -5 $O/b1080.err; exit 1; }
+  line $O/b1080.json
+  timeout -k 10 300 python3 bench.py --workload batch1080 --gpus 2 --allow-shared-gpu > $O/b1080x2.json 2> $O/b1080x2.err || { tail -5 $O/b1080x2.err; exit 1; }
+  line $O/b1080x2.json
+  timeout -k 10 300 python3 bench.py --width 16384 --height 16384 --frames 16 --steps 5 --warmup 1 --no-cpu-baseline --latency-calls 0 > $O/16k.json 2> $O/16k.err || { tail -5 $O/16k.err; exit 1; }
+  line $O/16k.json
+  ;;
+esac
 true
