@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             wave_order();
             if (j0 >= nb) continue;
             const uint32_t j1 = min(nb, j0 + 8u);
-            const int16_t* cp = st16 + natoff;  // (the pair after the chunk's last reads past it: unused)
+            const int16_t* cp = st16 + natoff;  // this lane's coefficient of the pair's first block
             uint32_t jb = j0;
             for (; jb + 1 < j1; jb += 2, cp += 128) {
                 const int cA = cp[0], cB = cp[64];
