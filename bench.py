@@ -242,11 +242,15 @@ def device_for(local: int) -> int:
     return local % max(1, visible_devices())
 
 
-def rank_lanes(args) -> int:
-    """Encoder lanes of this rank: --lanes, else the library default (4), also when ranks
-    share a GPU (--allow-shared-gpu): 2 ranks x 4 lanes ran config 4 at 0.81x one rank on
-    the GPU, 2 x 2 lanes at 0.74x (profiles/r05_bench_batch1080_x2.json)."""
-    return args.lanes
+def rank_lanes(args, world: int) -> int:
+    """Encoder lanes of this rank: --lanes, else the library default (4) on a GPU of its
+    own.  Ranks sharing a GPU (--allow-shared-gpu) split ~6 lanes between them: config 4
+    on 2 ranks sharing one GPU ran at 0.88x one rank on it with 3 lanes each, 0.82x with
+    4 and 0.74x with 2 (one box)."""
+    if args.lanes:
+        return args.lanes
+    per_device = -(-world // max(1, visible_devices()))
+    return max(1, 6 // per_device) if per_device > 1 else 0
 
 
 def gather_group(world: int):
@@ -588,7 +592,7 @@ def run_batch1080(args, rank, local, world, pg):
     host = {i: J.synth_rgb8(batch_seed(i), W, H) for i in share}
     ins = {i: torch.from_numpy(host[i].reshape(-1)).to(dev) for i in share}
     frames = [(ins[i].data_ptr(), W, H, W * 3) for i in share]
-    enc = J.Encoder(local, lanes=rank_lanes(args))
+    enc = J.Encoder(local, lanes=rank_lanes(args, world))
     gather, transport = None, None
     nsets = 1
     if world > 1 and not os.environ.get("JPGE_BENCH_NO_GATHER"):  # (diagnostic: encode only, no gather)
@@ -713,7 +717,7 @@ def run_frames(args, rank, local, world, pg):
     local = device_for(local)
     torch.cuda.set_device(local)
     dev = f"cuda:{local}"
-    enc = J.Encoder(local, lanes=rank_lanes(args))
+    enc = J.Encoder(local, lanes=rank_lanes(args, world))
     enc.set_subsampling(args.subsampling)
     W, H = args.width, args.height
     F = args.frames or 3072
