@@ -201,6 +201,7 @@ struct CtlLayout {
 };
 
 constexpr size_t kStatsDoneOff = 64;  // K2's finished-workgroup count: a line of its own in the `done` block
+constexpr size_t kPackDoneOff = 128;  // the pack kernel's count, end offset and flag: another line
 
 struct HostHist {  // written by hist_export_kernel into mapped pinned memory
     uint32_t cnt[4 * 256];  // replicas summed
@@ -944,8 +945,14 @@ int Encoder::import_tables_copy(Slot& s) {
 
 // Phase 2b (GPU): the entropy kernels (tables already on the device); `exp`: a
 // later frame whose histograms the code kernel exports on the way.
-int Encoder::launch_entropy_phase(Slot& s, Slot* exp) {
+int Encoder::launch_entropy_phase(Slot& s, Slot* exp, bool lone) {
     EntropyArgs e = entropy_args(s);
+    // A single image on a 1-lane encoder (encode()): the result is handed over once every
+    // pack workgroup's write-through stores have completed, so the call need not wait for
+    // the kernel's formal end (9 us per 4K call).  The pipeline streams its stores
+    // instead (write-through cost it 1.3%) and awaits its stream at the batch's end.
+    if (lone && lanes_.size() == 1)
+        e.pack_done = reinterpret_cast<uint32_t*>(s.d_ctl + CtlLayout(slot_layout(s).grid()).done + kPackDoneOff);
     s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1)
     e.exp_hist = exp ? exp->hist : HistPtrs{};
     e.exp_cnt = exp ? exp->d_hist_host->cnt : nullptr;
@@ -1018,17 +1025,24 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (!st) st = build_tables(s, false);
     if (lat_prof_) T[2] = clk::now();
     if (!st) st = import_tables_copy(s);
-    if (!st) st = launch_entropy_phase(s, nullptr);
+    if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true);
     if (lat_prof_) T[3] = clk::now();
     if (!st) st = finish(s, f, flags);
     if (lat_prof_) T[4] = clk::now();
-    // every output byte is in place: the stream's tail, awaited by spinning as a batch
-    // lane's end (a blocking stream synchronisation took ~9 us after the result word)
-    if (end_sync_ == 2 || hipEventRecord(lanes_[0]->done, s.stream) != hipSuccess) {
-        hipStreamSynchronize(s.stream);
-    } else {
-        const hipError_t w = end_sync_ == 1 ? hipEventSynchronize(lanes_[0]->done) : wait_event(lanes_[0]->done);
-        if (w != hipSuccess && !st) st = kErrHip;
+    // Every output byte is in place.  Device output on a 1-lane encoder: the result word is
+    // written once every pack workgroup's (write-through) stores have completed, so the
+    // kernel's formal end is not awaited (the stream orders the context's next work after
+    // it; ~9 us).  Host
+    // output: the copy queued by finish(), awaited by spinning as a batch lane's end (a
+    // blocking stream synchronisation adds tens of us of wake-up).
+    const bool await_end = st || !(flags & kFlagDeviceOutput) || end_sync_ != 0 || lanes_.size() != 1;
+    if (await_end) {
+        if (end_sync_ == 2 || hipEventRecord(lanes_[0]->done, s.stream) != hipSuccess) {
+            hipStreamSynchronize(s.stream);
+        } else {
+            const hipError_t w = end_sync_ == 1 ? hipEventSynchronize(lanes_[0]->done) : wait_event(lanes_[0]->done);
+            if (w != hipSuccess && !st) st = kErrHip;
+        }
     }
     if (lat_prof_ && !st) {
         T[5] = clk::now();

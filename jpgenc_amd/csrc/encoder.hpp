@@ -152,7 +152,7 @@ class Encoder {
     EntropyArgs entropy_args(Slot& s);
     // phase 2b (GPU): table upload (when not carried) + entropy kernels
     int import_tables_copy(Slot& s);
-    int launch_entropy_phase(Slot& s, Slot* exp);
+    int launch_entropy_phase(Slot& s, Slot* exp, bool lone = false);  // lone: encode()'s single image
     // idle: work the wait may do between its polls (returns whether it did any)
     int finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait = true, const std::function<bool()>* idle = nullptr);
     // one lane's software pipeline over the frames it takes from fr[0..total) through `next`

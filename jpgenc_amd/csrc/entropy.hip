@@ -42,6 +42,8 @@ constexpr int kStageWords = kK3Blocks * kStageBytesPerBlock / 4 + 4;  // worst-c
 constexpr int kWin = 32;                                              // output bytes per lane per round
 constexpr int kWinWords = kWin / 4;
 static_assert(kWinWords == 8 && kEntropyRegionBytes % 16 == 0, "pack loads a window as two aligned uint4");
+constexpr int kPackStoreAux = 16;  // sc1: write-through output stores (single-frame launches, pack_done)
+constexpr int kPackStoreNt = 2;    // nt: streaming output stores (the pipeline: write-through cost 1.3%)
 constexpr int kChunk = kK3Threads * kWin;                             // output bytes per round (pre-stuffing)
 
 // per-workgroup record handed from the code kernel to the pack kernel
@@ -621,9 +623,19 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
     const WgTiles wt = wg_tiles(a.seg, wg);
     const bool fills = a.rst.mcus ? wt.last : eoi;
     JPGE_STAMP(0);
+    // With pack_done (single-frame launches of a 1-lane encoder) every output byte is
+    // stored write-through (sc1), so once a workgroup's stores have completed its bytes
+    // are in memory, not in its XCD's L2; the pipeline streams them (nt).  Single bytes
+    // (headers, markers, EOI) are always written through.
+    const bool wthru = a.pack_done != nullptr;
+    const __amdgpu_buffer_rsrc_t out_rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.out, 0, (int)(a.out_cap < 0x7FFFFFF0ull ? a.out_cap : 0x7FFFFFF0ull), 0x00020000);
+    auto out_byte = [&](uint64_t i, uint32_t v) {  // (single bytes: headers, markers, EOI)
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rs, (uint32_t)i, 0, kPackStoreAux);
+    };
     if (wg == 0 && (a.flags & kStripeFirst)) {  // the headers (SOI .. SOS) travel behind the tables
         const uint8_t* hdr = reinterpret_cast<const uint8_t*>(a.tables + 1024);
-        for (uint32_t i = tid; i < a.hdr_len; i += kK3Threads) a.out[i] = hdr[i];
+        for (uint32_t i = tid; i < a.hdr_len; i += kK3Threads) out_byte(i, hdr[i]);
     }
 
     // ---- this workgroup's placement: from the scan kernel, or scanned here ----
@@ -666,8 +678,11 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
     const uint64_t ntot = (uint64_t)n_own + ftotal + (eoi ? 2u : 0u);
     const bool fits = D0 + ntot <= a.out_cap;
     if (fits && wt.first && markers && tid == 0) {  // RSTn ahead of the segment (not stuffed)
-        a.out[D0 - 2] = 0xFF;
-        a.out[D0 - 1] = (uint8_t)(0xD0 + ((a.seg_index0 + S.seg - 1) & 7));  // RST(interval - 1 mod 8)
+        uint8_t* const m = a.out + D0 - 2;
+        const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(m, 0, 2, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0xFF, mrs, 0, 0, kPackStoreAux);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(0xD0 + ((a.seg_index0 + S.seg - 1) & 7)), mrs, 1, 0,
+                                             kPackStoreAux);  // RST(interval - 1 mod 8)
     }
     const uint32_t split = S.split, fill = S.fill;
     const uint32_t* R32 = reinterpret_cast<const uint32_t*>(a.ubuf + (uint64_t)wg * kEntropyRegionBytes);
@@ -755,12 +770,16 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
         __syncthreads();
         uint8_t* gout = a.out + (d - align);
         const uint32_t nw = (align + clen + 3) / 4;
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(gout, 0, (int)(4 * nw), 0x00020000);
         for (uint32_t w = tid; w < nw; w += kK3Threads) {
             const uint32_t s = 4 * w, e = s + 4;
             if (s >= align && e <= align + clen) {
-                __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(S.ob + s), reinterpret_cast<uint32_t*>(gout + s));
+                const uint32_t v = *reinterpret_cast<const uint32_t*>(S.ob + s);
+                if (wthru) __builtin_amdgcn_raw_buffer_store_b32(v, ors, s, 0, kPackStoreAux);
+                else __builtin_amdgcn_raw_buffer_store_b32(v, ors, s, 0, kPackStoreNt);
             } else {
-                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q) gout[q] = S.ob[q];
+                for (uint32_t q = max(s, align); q < min(e, align + clen); ++q)
+                    __builtin_amdgcn_raw_buffer_store_b8(S.ob[q], ors, q, 0, kPackStoreAux);
             }
         }
         d += clen;
@@ -770,18 +789,42 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
         uint64_t len = 0;  // end of the image (EOI written) or of the stripe's bytes
         if (fits) {
             if (eoi) {  // EOI, Image.cpp:1003-1005
-                a.out[d] = 0xFF;
-                a.out[d + 1] = 0xD9;
+                uint8_t* const m = a.out + d;
+                const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(m, 0, 2, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0xFF, mrs, 0, 0, kPackStoreAux);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0xD9, mrs, 1, 0, kPackStoreAux);
                 d += 2;
             }
             len = d;
         }
-        // length and no-space flag straight into mapped host memory: the last
-        // workgroup's end offset bounds every workgroup's, so it alone decides
-        // whether the output fits (no fence needed: the host reads after the kernel)
-        __hip_atomic_store(&a.host_result[0], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.host_result[1], fits ? 0ull : 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.host_result[3], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the last workgroup's end offset bounds every workgroup's, so it alone decides
+        // whether the output fits
+        if (a.pack_done) {  // (left for the last workgroup to finish)
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(a.pack_done + 2), len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.pack_done + 4, fits ? 0u : 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (a.host_result) {  // (no fence needed: the host reads after the kernel)
+            __hip_atomic_store(&a.host_result[0], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.host_result[1], fits ? 0ull : 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.host_result[3], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (a.pack_done) {
+        // The length, flags and sequence word go into mapped host memory once EVERY
+        // workgroup's output stores have completed (each counts itself after them; they
+        // are write-through, so complete means in memory): the host may then use the
+        // bytes before the kernel has formally ended.
+        vm_drain();
+        __syncthreads();
+        if (tid == 0 && atomicAdd(a.pack_done, 1u) == G - 1 && a.host_result) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the last workgroup's end offset)
+            const uint64_t len =
+                __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.pack_done + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t nospace = __hip_atomic_load(a.pack_done + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.pack_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (reusable without K1)
+            __hip_atomic_store(&a.host_result[0], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.host_result[1], (uint64_t)nospace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.host_result[3], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     JPGE_STAMP(2);
 }

@@ -219,8 +219,12 @@ struct EntropyArgs {
     uint8_t* ubuf;           // per-workgroup unstuffed regions (entropy_ubuf_bytes)
     uint8_t* rec;            // [entropy_grid][kEntropyRecordBytes] code -> pack kernel records
     uint32_t* done = nullptr;  // (zeroed per frame) code workgroups finished: the last one places all
+    // (zeroed per frame) pack workgroups finished, then the last workgroup's end offset
+    // (u64 at [2]) and no-space flag ([4]): the last to finish hands the result over
+    uint32_t* pack_done = nullptr;
     uint64_t* host_result;   // mapped pinned host memory: [0] .jpg bytes, [1] no-space (4),
-                             // [2] reserved (0), [3] = seq, written last
+                             // [2] reserved (0), [3] = seq, written last, once every
+                             // workgroup's output stores have completed (pack_done)
     uint64_t seq;            // the frame's sequence number
     // carried duty of the code kernel: export another frame's histograms to mapped
     // host memory (workgroup 0; exp_cnt == nullptr: none)
