@@ -560,6 +560,9 @@ Encoder::~Encoder() {
                      lat_ns_[0] / 1e3 / lat_calls_, lat_ns_[1] / 1e3 / lat_calls_, lat_ns_[2] / 1e3 / lat_calls_,
                      lat_ns_[3] / 1e3 / lat_calls_, lat_ns_[4] / 1e3 / lat_calls_, lat_ns_[5] / 1e3 / lat_calls_,
                      (long long)lat_calls_);
+    if (lat_prof_ && lat_calls_)
+        std::fprintf(stderr, "jpge   of launch-1: argument preparation %.2f, K1 launch %.2f\n", lat_ns_[6] / 1e3 / lat_calls_,
+                     lat_ns_[7] / 1e3 / lat_calls_);
     if (cpu_prof_ && cpu_frames_.load()) {
         const double f = (double)cpu_frames_.load();
         std::fprintf(stderr, "jpge cpu per frame (us): tables %.2f launch-1 %.2f launch-entropy %.2f finish %.2f "
@@ -805,12 +808,15 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
                     Slot* imp, bool export_hist) {
     FdctArgs a;
     StatsArgs st2;
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = lat_prof_ ? clk::now() : clk::time_point{};
     if (const int st = prep1(s, f, qy, qc, flags, imp, a, st2)) return st;
+    const clk::time_point t1 = lat_prof_ ? clk::now() : clk::time_point{};
     s.timed = timing_every_ && (frame_counter_++ % (uint64_t)timing_every_) == 0;
     s.timed_frames = 1;
     s.count_symbols = s.timed;
     // sampled frames: each kernel launched with its own events (KTimer, kernels.hpp)
-    const KTimer t1{s.ev[0], s.ev[1]}, t2{s.ev[2], s.ev[3]};
+    const KTimer t1k{s.ev[0], s.ev[1]}, t2k{s.ev[2], s.ev[3]};
     s.seq = ++seq_counter_;
     s.hist = st2.hist;
     if (export_hist) {  // (by K2's last workgroup: no launch of its own)
@@ -820,9 +826,14 @@ int Encoder::phase1(Slot& s, const FrameDesc& f, const uint8_t qy[64], const uin
         st2.host_seq = &s.d_hist_host->seq;
         st2.seq = s.seq;
     }
-    JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1 : nullptr));
-    JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2 : nullptr));
+    JPGE_HIP(launch_fdct(a, s.stream, s.timed ? &t1k : nullptr));
+    const clk::time_point t2 = lat_prof_ ? clk::now() : clk::time_point{};
+    JPGE_HIP(launch_stats(st2, s.stream, s.timed ? &t2k : nullptr));
     if (export_hist) s.export_queued.store(1, std::memory_order_release);
+    if (lat_prof_) {
+        lat_ns_[6] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+        lat_ns_[7] += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+    }
     return kOk;
 }
 

@@ -213,7 +213,7 @@ class Encoder {
     std::atomic<int64_t> cpu_read_ns_{0}, cpu_build_ns_{0}, cpu_builds_{0}, cpu_part_ns_[3] = {};
     int hist_nap_us_ = 0;    // a single lane's histogram wait: nap between polls (0: spin, for latency)
     bool lat_prof_ = false;  // JPGE_LAT_PROF: single-frame encode() phases, wall time (printed at close)
-    int64_t lat_ns_[6] = {}, lat_calls_ = 0;
+    int64_t lat_ns_[8] = {}, lat_calls_ = 0;  // (6, 7: phase1's argument preparation, K1 launch)
     std::chrono::steady_clock::time_point lat_hist_seen_{};
     const char* stamps_file_ = nullptr;  // JPGE_STAMPS_FILE: dump diagnostic phase stamps (diag builds)
     uint64_t* d_dbg_ = nullptr;
