@@ -134,7 +134,12 @@ size_t jpge_max_jpeg_bytes(uint32_t width, uint32_t height);
 int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]);
 
 /* Full encode — replaces Image::writeJPEG (Image.hpp:92, Image.cpp:831-976) for an
- * image as produced by loadPPM: SOI APP0 DQT DQT SOF0 DHTx4 SOS <entropy> EOI. */
+ * image as produced by loadPPM: SOI APP0 DQT DQT SOF0 DHTx4 SOS <entropy> EOI.
+ * Returns once every output byte is in place: in host memory (host output), or in
+ * device memory (JPGE_DEVICE_OUTPUT), readable from any stream.  On a 1-lane context
+ * with device output the call returns as soon as the bytes are written, while the
+ * context's stream may still be retiring the last kernel (later work on the context
+ * is ordered after it). */
 int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t width, uint32_t height, size_t stride,
                      int maxval, const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap,
                      size_t* len, uint32_t flags);
