@@ -882,14 +882,10 @@ int Encoder::build_tables(Slot& s, bool parallel) {
         return (int64_t)t.tv_sec * 1000000000 + t.tv_nsec;
     };
     const int64_t t0 = cpu_prof_ ? thread_ns() : 0;
-    uint32_t cnt[1024];
-    uint64_t first[1024];
-    for (int i = 0; i < 1024; ++i) {
-        cnt[i] = s.h_hist->cnt[i];
-        first[i] = ~s.h_hist->key[i];
-    }
+    // (the tables read the mapped export in place: the keys stay inverted, and only the
+    // present symbols' keys are read)
     const int64_t t1 = cpu_prof_ ? thread_ns() : 0;
-    const int r = build_tables_from(s, cnt, first, parallel);
+    const int r = build_tables_from(s, s.h_hist->cnt, s.h_hist->key, parallel, /*inverted=*/true);
     if (cpu_prof_) {
         cpu_read_ns_.fetch_add(t1 - t0, std::memory_order_relaxed);
         cpu_build_ns_.fetch_add(thread_ns() - t1, std::memory_order_relaxed);
@@ -900,7 +896,8 @@ int Encoder::build_tables(Slot& s, bool parallel) {
 
 // The four tables from counts and first-occurrence keys, and the headers (the
 // image's real dimensions in SOF0), into the slot's pinned staging buffer.
-int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t* first_all, bool parallel) {
+int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t* first_all, bool parallel,
+                               bool inverted) {
     auto thread_ns = [] {
         timespec t;
         clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
@@ -910,7 +907,10 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     HuffTable tabs[4];
     int ok[4] = {0, 0, 0, 0};
     // the four tables are independent; the AC tables dominate
-    parallel_for(4, parallel ? 4 : 1, [&](long t) { ok[t] = build_table(cnt_all + t * 256, first_all + t * 256, tabs[t]); });
+    parallel_for(4, parallel ? 4 : 1, [&](long t) {
+        ok[t] = inverted ? build_table_inverted(cnt_all + t * 256, first_all + t * 256, tabs[t])
+                         : build_table(cnt_all + t * 256, first_all + t * 256, tabs[t]);
+    });
     const int64_t t1 = cpu_prof_ ? thread_ns() : 0;
     for (int t = 0; t < 4; ++t)
         if (ok[t])

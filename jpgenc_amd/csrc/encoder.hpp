@@ -146,7 +146,8 @@ class Encoder {
     int add_slots(Lane& ln, int count);
     // phase 2a (host, any thread): Huffman tables + headers from the histograms
     int build_tables(Slot& s, bool parallel);
-    int build_tables_from(Slot& s, const uint32_t* cnt, const uint64_t* first, bool parallel);
+    int build_tables_from(Slot& s, const uint32_t* cnt, const uint64_t* first, bool parallel,
+                          bool inverted = false);  // inverted: first holds ~keys (the device export)
     FdctArgs fdct_args(Slot& s, int maxval, Slot* imp);
     StatsArgs stats_args(Slot& s);
     EntropyArgs entropy_args(Slot& s);

@@ -751,14 +751,16 @@ bool build_table_std(const uint32_t counts[256], const uint64_t first_key[256], 
     return build_table_with(counts, first_key, out, build_code_lengths_std);
 }
 
-bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out) {
-    if (!HashOrder::usable()) return build_table_std(counts, first_key, out);
+// kInv: the keys arrive inverted (~first occurrence: the device's atomicMax form, read
+// straight from the mapped histogram export)
+template <bool kInv>
+static bool build_table_impl(const uint32_t counts[256], const uint64_t keys[256], HuffTable& out) {
     // symbols in first-occurrence order
     uint64_t key[kMaxSyms];
     int syms[kMaxSyms], cnts[kMaxSyms], n = 0;
     for (int s = 0; s < 256; ++s)
         if (counts[s]) {
-            key[n] = (first_key[s] << 8) | (uint64_t)s;  // (keys are < 2^56: text positions)
+            key[n] = ((kInv ? ~keys[s] : keys[s]) << 8) | (uint64_t)s;  // (keys are < 2^56: text positions)
             ++n;
         }
     if (!n) return false;
@@ -785,6 +787,20 @@ bool build_table(const uint32_t counts[256], const uint64_t first_key[256], Huff
     }
     out.nsym = k;
     return true;
+}
+
+bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out) {
+    if (!HashOrder::usable()) return build_table_std(counts, first_key, out);
+    return build_table_impl<false>(counts, first_key, out);
+}
+
+bool build_table_inverted(const uint32_t counts[256], const uint64_t inv_key[256], HuffTable& out) {
+    if (!HashOrder::usable()) {
+        uint64_t first[256];
+        for (int s = 0; s < 256; ++s) first[s] = ~inv_key[s];
+        return build_table_std(counts, first, out);
+    }
+    return build_table_impl<true>(counts, inv_key, out);
 }
 
 std::pair<std::vector<std::pair<int, GenericCode>>, std::vector<std::vector<int>>>

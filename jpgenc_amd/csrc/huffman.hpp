@@ -39,6 +39,8 @@ std::vector<std::pair<int, GenericCode>> assign_codes(const std::vector<std::vec
 // (keys are any totally ordered u64; absent symbols have counts[s] == 0).
 // Returns false if every count is zero.
 bool build_table(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out);
+// The same with inverted keys (inv_key[s] = ~first_key[s]: the device export's form).
+bool build_table_inverted(const uint32_t counts[256], const uint64_t inv_key[256], HuffTable& out);
 // The same table through std::unordered_map / std::priority_queue themselves (the
 // containers the reference uses; test cross-check of build_table's array emulation).
 bool build_table_std(const uint32_t counts[256], const uint64_t first_key[256], HuffTable& out);
