@@ -306,6 +306,87 @@ class Encoder::TablePool {
     double ready_dev_ = 0;  // smoothed |delay - ready_us_|
 };
 
+// A 1-lane encoder's second table thread, for single images (encode()): while the calling
+// thread builds the luma AC table (the largest: ~2/3 of a frame's table time), it builds
+// the other three.  It is armed when a call starts waiting for its histograms (so its
+// wake-up overlaps the two kernels), spins only until the call's tables are built, and
+// otherwise sleeps on a condition variable.
+class Encoder::TableHelper {
+  public:
+    TableHelper() {
+        th_ = std::thread([this] {
+            prctl(PR_SET_NAME, "jpge-tables", 0, 0, 0);
+            run();
+        });
+    }
+    ~TableHelper() {
+        state_.store(kStop, std::memory_order_release);
+        { std::lock_guard<std::mutex> g(mu_); }
+        cv_.notify_one();
+        th_.join();
+    }
+    void arm() {
+        int idle = kIdle;
+        if (state_.compare_exchange_strong(idle, kArmed, std::memory_order_acq_rel)) {
+            { std::lock_guard<std::mutex> g(mu_); }
+            cv_.notify_one();
+        }
+    }
+    void disarm() {
+        int s = state_.load(std::memory_order_acquire);
+        while ((s == kArmed || s == kDone) && !state_.compare_exchange_weak(s, kIdle, std::memory_order_acq_rel)) {
+        }
+    }
+    // tables 0, 2 and 3 (DC luma, DC and AC chroma) on the helper; false: not armed (the
+    // caller builds them itself)
+    bool post(const uint32_t* cnt, const uint64_t* key, bool inverted, HuffTable* tabs, int* ok) {
+        if (state_.load(std::memory_order_acquire) != kArmed) return false;
+        cnt_ = cnt;
+        key_ = key;
+        inv_ = inverted;
+        tabs_ = tabs;
+        ok_ = ok;
+        int armed = kArmed;
+        return state_.compare_exchange_strong(armed, kJob, std::memory_order_acq_rel);
+    }
+    void wait() {
+        while (state_.load(std::memory_order_acquire) != kDone) __builtin_ia32_pause();
+    }
+
+  private:
+    enum { kIdle, kArmed, kJob, kDone, kStop };
+    void run() {
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return state_.load(std::memory_order_acquire) != kIdle; });
+            }
+            for (;;) {
+                const int s = state_.load(std::memory_order_acquire);
+                if (s == kStop) return;
+                if (s == kIdle) break;
+                if (s == kJob) {
+                    for (int t : {0, 2, 3})
+                        ok_[t] = inv_ ? build_table_inverted(cnt_ + t * 256, key_ + t * 256, tabs_[t])
+                                      : build_table(cnt_ + t * 256, key_ + t * 256, tabs_[t]);
+                    state_.store(kDone, std::memory_order_release);
+                    continue;
+                }
+                __builtin_ia32_pause();
+            }
+        }
+    }
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::atomic<int> state_{kIdle};
+    const uint32_t* cnt_ = nullptr;
+    const uint64_t* key_ = nullptr;
+    bool inv_ = false;
+    HuffTable* tabs_ = nullptr;
+    int* ok_ = nullptr;
+};
+
 struct Encoder::Slot {
     hipStream_t stream = nullptr;  // the encoder's stream (shared by all slots, not owned)
     // 0-2, 4-5 kernel timing brackets (3, 6, 7 unused)
@@ -469,6 +550,7 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->host_trace_file_ = std::getenv("JPGE_HOST_TRACE");
     e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
     e->lat_prof_ = env_int("JPGE_LAT_PROF", 0, 0, 1) != 0;
+    e->table_helper_ = env_int("JPGE_TABLE_HELPER", 1, 0, 1) != 0;
     e->hist_nap_us_ = env_int("JPGE_HIST_NAP_US", e->hist_nap_us_, 0, 1000);
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
@@ -584,6 +666,7 @@ Encoder::~Encoder() {
                              (unsigned long long)g->ready, g->waits ? (double)g->naps / g->waits : 0.0,
                              g->waits ? g->total_us / g->waits : 0.0, g->ema_us);
     }
+    helper_.reset();
     for (auto& ln : lanes_) ln->shutdown();
     for (auto& b : scratch_) hipFree(b.first);
     pool_.reset();  // (no jobs are pending between calls)
@@ -871,7 +954,7 @@ int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a_in, const Stats
 // Phase 2a (host; the calling thread or a pool worker): wait for the histograms,
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
-int Encoder::build_tables(Slot& s, bool parallel) {
+int Encoder::build_tables(Slot& s, bool parallel, TableHelper* helper) {
     if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : hist_nap_us_), &s.export_queued,
                                s.inline_tables ? s.guess_hist : nullptr))
         return w;
@@ -885,7 +968,7 @@ int Encoder::build_tables(Slot& s, bool parallel) {
     // (the tables read the mapped export in place: the keys stay inverted, and only the
     // present symbols' keys are read)
     const int64_t t1 = cpu_prof_ ? thread_ns() : 0;
-    const int r = build_tables_from(s, s.h_hist->cnt, s.h_hist->key, parallel, /*inverted=*/true);
+    const int r = build_tables_from(s, s.h_hist->cnt, s.h_hist->key, parallel, /*inverted=*/true, helper);
     if (cpu_prof_) {
         cpu_read_ns_.fetch_add(t1 - t0, std::memory_order_relaxed);
         cpu_build_ns_.fetch_add(thread_ns() - t1, std::memory_order_relaxed);
@@ -897,7 +980,7 @@ int Encoder::build_tables(Slot& s, bool parallel) {
 // The four tables from counts and first-occurrence keys, and the headers (the
 // image's real dimensions in SOF0), into the slot's pinned staging buffer.
 int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t* first_all, bool parallel,
-                               bool inverted) {
+                               bool inverted, TableHelper* helper) {
     auto thread_ns = [] {
         timespec t;
         clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
@@ -907,10 +990,16 @@ int Encoder::build_tables_from(Slot& s, const uint32_t* cnt_all, const uint64_t*
     HuffTable tabs[4];
     int ok[4] = {0, 0, 0, 0};
     // the four tables are independent; the AC tables dominate
-    parallel_for(4, parallel ? 4 : 1, [&](long t) {
+    auto one = [&](long t) {
         ok[t] = inverted ? build_table_inverted(cnt_all + t * 256, first_all + t * 256, tabs[t])
                          : build_table(cnt_all + t * 256, first_all + t * 256, tabs[t]);
-    });
+    };
+    if (helper && helper->post(cnt_all, first_all, inverted, tabs, ok)) {
+        one(1);  // (the luma AC table here, the other three on the helper)
+        helper->wait();
+    } else {
+        parallel_for(4, parallel ? 4 : 1, one);
+    }
     const int64_t t1 = cpu_prof_ ? thread_ns() : 0;
     for (int t = 0; t < 4; ++t)
         if (ok[t])
@@ -1031,9 +1120,17 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (lat_prof_) T[0] = clk::now();
     int st = phase1(s, f, qy, qc, flags, nullptr, true);
     if (lat_prof_) T[1] = clk::now();
-    // (serially: spawning threads for the four tables costs more than the ~14 us of a 4K
-    // frame's tables they would overlap)
-    if (!st) st = build_tables(s, false);
+    // The tables: on this thread, with the helper thread of a 1-lane encoder for frames
+    // of 1 MPix and up (armed now, so its wake-up overlaps the kernels; spawning threads
+    // per call would cost more than the tables it overlaps)
+    TableHelper* helper = nullptr;
+    if (!st && table_helper_ && lanes_.size() == 1 && (uint64_t)f.width * f.height >= (1u << 20)) {
+        if (!helper_) helper_.reset(new TableHelper());
+        helper = helper_.get();
+        helper->arm();
+    }
+    if (!st) st = build_tables(s, false, helper);
+    if (helper) helper->disarm();
     if (lat_prof_) T[2] = clk::now();
     if (!st) st = import_tables_copy(s);
     if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true);

@@ -127,6 +127,7 @@ class Encoder {
     struct Slot;
     struct Lane;
     class TablePool;
+    class TableHelper;
     Encoder() = default;
     int ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap);
     // phase 1 (GPU): upload, transform + statistics kernels, histogram download
@@ -145,9 +146,10 @@ class Encoder {
     // a lane's slots: at least `count`
     int add_slots(Lane& ln, int count);
     // phase 2a (host, any thread): Huffman tables + headers from the histograms
-    int build_tables(Slot& s, bool parallel);
+    int build_tables(Slot& s, bool parallel, TableHelper* helper = nullptr);
     int build_tables_from(Slot& s, const uint32_t* cnt, const uint64_t* first, bool parallel,
-                          bool inverted = false);  // inverted: first holds ~keys (the device export)
+                          bool inverted = false,  // inverted: first holds ~keys (the device export)
+                          TableHelper* helper = nullptr);  // (builds three of the four tables)
     FdctArgs fdct_args(Slot& s, int maxval, Slot* imp);
     StatsArgs stats_args(Slot& s);
     EntropyArgs entropy_args(Slot& s);
@@ -166,6 +168,8 @@ class Encoder {
     std::atomic<uint64_t> frame_counter_{0};
     std::atomic<uint64_t> seq_counter_{0};
     std::unique_ptr<TablePool> pool_;
+    std::unique_ptr<TableHelper> helper_;  // single images on a 1-lane encoder: a second table thread
+    bool table_helper_ = true;             // JPGE_TABLE_HELPER=0: none
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
