@@ -411,6 +411,7 @@ struct Encoder::Slot {
     uint32_t* h_tab = nullptr;     // same layout as d_tab (mapped)
     uint32_t* d_tab_host = nullptr;  // device view of h_tab
     uint64_t* h_result = nullptr;  // mapped: written by the entropy kernel's last workgroup
+                                   // ([0, 4)); [6]: encode()'s gate word (gate())
     uint64_t* d_result_host = nullptr;
     // per-frame state between phases
     const uint8_t* in_dev = nullptr;
@@ -439,6 +440,8 @@ struct Encoder::Slot {
     // the lane's wait estimates (histograms when its own thread builds the tables; results)
     WaitGuess* guess_hist = nullptr;
     WaitGuess* guess_result = nullptr;
+
+    uint32_t* gate() const { return reinterpret_cast<uint32_t*>(h_result + 6); }
 
     ~Slot() {
         hipFree(d_in); hipFree(d_coef); hipFree(d_ctl); hipFree(d_ubuf);
@@ -551,6 +554,12 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
     e->lat_prof_ = env_int("JPGE_LAT_PROF", 0, 0, 1) != 0;
     e->table_helper_ = env_int("JPGE_TABLE_HELPER", 1, 0, 1) != 0;
+    {
+        int wv = 0;
+        e->gate_ = env_int("JPGE_GATE", 1, 0, 1) != 0 &&
+                   hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv;
+        (void)hipGetLastError();
+    }
     e->hist_nap_us_ = env_int("JPGE_HIST_NAP_US", e->hist_nap_us_, 0, 1000);
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
@@ -627,7 +636,11 @@ int Encoder::add_slots(Lane& ln, int count) {
         JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_hist_host, s->h_hist, 0));
         JPGE_HIP(hipHostMalloc((void**)&s->h_tab, kTabBytes + kHdrMax, hipHostMallocMapped));
         JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_tab_host, s->h_tab, 0));
+        // (zeroed: a code kernel behind encode()'s gate reads whatever tables are here when
+        // a table build fails, and zero lengths keep it within its bounds)
+        std::memset(s->h_tab, 0, kTabBytes + kHdrMax);
         JPGE_HIP(hipHostMalloc((void**)&s->h_result, 64, hipHostMallocMapped));
+        std::memset(s->h_result, 0, 64);
         JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
         JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
         ln.slots.push_back(std::move(s));
@@ -1045,7 +1058,7 @@ int Encoder::import_tables_copy(Slot& s) {
 
 // Phase 2b (GPU): the entropy kernels (tables already on the device); `exp`: a
 // later frame whose histograms the code kernel exports on the way.
-int Encoder::launch_entropy_phase(Slot& s, Slot* exp, bool lone) {
+int Encoder::launch_entropy_phase(Slot& s, Slot* exp, bool lone, int parts) {
     EntropyArgs e = entropy_args(s);
     // A single image on a 1-lane encoder (encode()): the result is handed over once every
     // pack workgroup's write-through stores have completed, so the call need not wait for
@@ -1060,7 +1073,8 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp, bool lone) {
     e.exp_seq = exp ? &exp->d_hist_host->seq : nullptr;
     e.exp_seqv = exp ? exp->seq : 0;
     const KTimer tc{s.ev[4], s.ev[5]}, tp{s.ev[6], s.ev[7]};
-    JPGE_HIP(launch_entropy(e, s.stream, s.timed ? &tc : nullptr, s.timed ? &tp : nullptr));
+    if (parts & 1) JPGE_HIP(launch_entropy_code(e, s.stream, s.timed ? &tc : nullptr));
+    if (parts & 2) JPGE_HIP(launch_entropy_pack(e, s.stream, s.timed ? &tp : nullptr));
     return kOk;
 }
 
@@ -1119,6 +1133,30 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     clk::time_point T[6];
     if (lat_prof_) T[0] = clk::now();
     int st = phase1(s, f, qy, qc, flags, nullptr, true);
+    // The gate: the tables' copy and the code kernel are queued now, behind a stream wait
+    // on a mapped word the host sets once the tables are in h_tab, so their launches
+    // overlap K1 and K2 instead of following the tables (the pack kernel's arguments
+    // carry the header length, so it is launched after them, while the code kernel
+    // runs).  Every path below opens the gate.  (A failed table build: the code kernel
+    // reads the tables h_tab holds, valid ones or zeros, and its output is discarded.)
+    uint32_t* const gate = s.gate();
+    const uint32_t gate_v = (uint32_t)s.seq;  // (differs from the previous call's value)
+    bool gated = false;
+    auto open_gate = [&] {
+        if (gated) __atomic_store_n(gate, gate_v, __ATOMIC_RELEASE);
+        gated = false;
+    };
+    if (!st && gate_) {
+        if (hipStreamWaitValue32(s.stream, gate, gate_v, hipStreamWaitValueEq, 0xFFFFFFFFu) == hipSuccess) {
+            gated = true;
+            if (hipMemcpyAsync(s.d_tab, s.h_tab, kTabBytes + kHdrMax, hipMemcpyHostToDevice, s.stream) != hipSuccess)
+                st = kErrHip;
+            if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/1);
+            if (st) open_gate();
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     if (lat_prof_) T[1] = clk::now();
     // The tables: on this thread, with the helper thread of a 1-lane encoder for frames
     // of 1 MPix and up (armed now, so its wake-up overlaps the kernels; spawning threads
@@ -1132,8 +1170,13 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (!st) st = build_tables(s, false, helper);
     if (helper) helper->disarm();
     if (lat_prof_) T[2] = clk::now();
-    if (!st) st = import_tables_copy(s);
-    if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true);
+    if (gated) {
+        open_gate();
+        if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/2);
+    } else {
+        if (!st) st = import_tables_copy(s);
+        if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true);
+    }
     if (lat_prof_) T[3] = clk::now();
     if (!st) st = finish(s, f, flags);
     if (lat_prof_) T[4] = clk::now();

@@ -155,7 +155,8 @@ class Encoder {
     EntropyArgs entropy_args(Slot& s);
     // phase 2b (GPU): table upload (when not carried) + entropy kernels
     int import_tables_copy(Slot& s);
-    int launch_entropy_phase(Slot& s, Slot* exp, bool lone = false);  // lone: encode()'s single image
+    // lone: encode()'s single image; parts: 1 the code kernel, 2 the pack kernel, 3 both
+    int launch_entropy_phase(Slot& s, Slot* exp, bool lone = false, int parts = 3);
     // idle: work the wait may do between its polls (returns whether it did any)
     int finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait = true, const std::function<bool()>* idle = nullptr);
     // one lane's software pipeline over the frames it takes from fr[0..total) through `next`
@@ -170,6 +171,7 @@ class Encoder {
     std::unique_ptr<TablePool> pool_;
     std::unique_ptr<TableHelper> helper_;  // single images on a 1-lane encoder: a second table thread
     bool table_helper_ = true;             // JPGE_TABLE_HELPER=0: none
+    bool gate_ = true;  // encode()'s gate (JPGE_GATE=0, or no device support: none)
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)

@@ -876,9 +876,18 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
 }
 
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tcode, const KTimer* tpack) {
+    const hipError_t e = launch_entropy_code(a, s, tcode);
+    return e != hipSuccess ? e : launch_entropy_pack(a, s, tpack);
+}
+
+hipError_t launch_entropy_code(const EntropyArgs& a, hipStream_t s, const KTimer* tcode) {
     const uint32_t G = a.seg.grid();
-    hipError_t e = launch_timed(tcode, entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&a, 1, G));
-    if (e != hipSuccess) return e;
+    return launch_timed(tcode, entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&a, 1, G));
+}
+
+hipError_t launch_entropy_pack(const EntropyArgs& a, hipStream_t s, const KTimer* tpack) {
+    const uint32_t G = a.seg.grid();
+    hipError_t e = hipSuccess;
     EntropyArgs b = a;
     b.dbg = a.dbg ? a.dbg + 65536 * kStampSlots : nullptr;  // (diag builds: the pack kernel's stamps)
     if (a.done) {  // placed by the code kernel's last workgroup

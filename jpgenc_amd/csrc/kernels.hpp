@@ -371,6 +371,10 @@ hipError_t launch_hist_export(const HistPtrs& h, uint32_t* host_cnt, uint64_t* h
 // code + pack kernels (with the placement scan between them when kExtPlace)
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* code = nullptr,
                           const KTimer* pack = nullptr);
+// its two halves: the code kernel does not read hdr_len, so it can be queued before the
+// header is known (encoder.cpp, encode()'s gate); the pack kernel (and placement)
+hipError_t launch_entropy_code(const EntropyArgs& a, hipStream_t s, const KTimer* code = nullptr);
+hipError_t launch_entropy_pack(const EntropyArgs& a, hipStream_t s, const KTimer* pack = nullptr);
 // stripes: code kernel + summary scan; then placement scan + pack kernel
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s);
 hipError_t launch_entropy_place_pack(const EntropyArgs& a, hipStream_t s);

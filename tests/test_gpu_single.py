@@ -4,7 +4,12 @@ result over once every workgroup's write-through stores have completed, and the 
 returns without waiting for the kernel's formal end (encoder.cpp encode(), entropy.hip
 pack_done).  The bytes must then be readable at once from another stream: each call's
 output buffer is poisoned first, read back on torch's stream right after the call and
-compared with the oracle; host output and a frame too big for its buffer as well."""
+compared with the oracle; host output and a frame too big for its buffer as well.
+
+The tables' copy and the code kernel wait behind a stream gate the host opens once the
+tables are built (encode()'s gate); a call that fails after queueing them (the header
+does not fit the buffer) must still open it, and the context must keep working.  With
+JPGE_GATE=0 the same bytes come from the ungated launches."""
 import numpy as np
 import pytest
 
@@ -48,3 +53,30 @@ def test_device_output_too_small(lone):
     with pytest.raises(J.JpgeError):
         lone.encode_ptr(d_in.data_ptr(), w, h, w * 3, out.data_ptr(), out.numel(), quality=100)
     assert lone.encode(rgb, quality=90) == _oracle.encode(rgb, 90)  # the context still works
+
+
+def test_header_does_not_fit(lone):
+    import torch
+
+    w, h = 320, 240
+    rgb = J.synth_rgb8(9, w, h)
+    d_in = torch.from_numpy(rgb.reshape(-1)).cuda()
+    out = torch.empty(64, dtype=torch.uint8, device="cuda")  # (a header takes ~600 bytes)
+    for _ in range(2):
+        with pytest.raises(J.JpgeError):
+            lone.encode_ptr(d_in.data_ptr(), w, h, w * 3, out.data_ptr(), out.numel(), quality=90)
+    cap = J.max_jpeg_bytes(w, h)
+    big = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    n = lone.encode_ptr(d_in.data_ptr(), w, h, w * 3, big.data_ptr(), cap, quality=90)
+    assert big[:n].cpu().numpy().tobytes() == _oracle.encode(rgb, 90)
+
+
+def test_gate_off_same_bytes(monkeypatch):
+    monkeypatch.setenv("JPGE_GATE", "0")
+    enc = J.Encoder(0, lanes=1)
+    try:
+        for w, h, q in [(1920, 1080, 90), (200, 136, 50)]:
+            rgb = J.synth_rgb8(31 + w, w, h)
+            assert enc.encode(rgb, quality=q) == _oracle.encode(rgb, q)
+    finally:
+        enc.close()
