@@ -1139,20 +1139,23 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     // carry the header length, so it is launched after them, while the code kernel
     // runs).  Every path below opens the gate.  (A failed table build: the code kernel
     // reads the tables h_tab holds, valid ones or zeros, and its output is discarded.)
-    uint32_t* const gate = s.gate();
-    const uint32_t gate_v = (uint32_t)s.seq;  // (differs from the previous call's value)
-    bool gated = false;
-    auto open_gate = [&] {
-        if (gated) __atomic_store_n(gate, gate_v, __ATOMIC_RELEASE);
-        gated = false;
-    };
+    struct Gate {  // (opened at the latest when the call unwinds)
+        uint32_t* word;
+        uint32_t value;  // (the frame's sequence number: differs from the previous call's)
+        bool shut = false;
+        void open() {
+            if (shut) __atomic_store_n(word, value, __ATOMIC_RELEASE);
+            shut = false;
+        }
+        ~Gate() { open(); }
+    } gate{s.gate(), (uint32_t)s.seq};
     if (!st && gate_) {
-        if (hipStreamWaitValue32(s.stream, gate, gate_v, hipStreamWaitValueEq, 0xFFFFFFFFu) == hipSuccess) {
-            gated = true;
+        if (hipStreamWaitValue32(s.stream, gate.word, gate.value, hipStreamWaitValueEq, 0xFFFFFFFFu) == hipSuccess) {
+            gate.shut = true;
             if (hipMemcpyAsync(s.d_tab, s.h_tab, kTabBytes + kHdrMax, hipMemcpyHostToDevice, s.stream) != hipSuccess)
                 st = kErrHip;
             if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/1);
-            if (st) open_gate();
+            if (st) gate.open();
         } else {
             (void)hipGetLastError();
         }
@@ -1170,8 +1173,8 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (!st) st = build_tables(s, false, helper);
     if (helper) helper->disarm();
     if (lat_prof_) T[2] = clk::now();
-    if (gated) {
-        open_gate();
+    if (gate.shut) {
+        gate.open();
         if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/2);
     } else {
         if (!st) st = import_tables_copy(s);
