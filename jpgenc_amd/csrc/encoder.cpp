@@ -554,10 +554,10 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->cpu_prof_ = env_int("JPGE_CPU_PROF", 0, 0, 1) != 0;
     e->lat_prof_ = env_int("JPGE_LAT_PROF", 0, 0, 1) != 0;
     e->table_helper_ = env_int("JPGE_TABLE_HELPER", 1, 0, 1) != 0;
-    {
+    e->gate_ = env_int("JPGE_GATE", 1, 0, 2);
+    if (e->gate_ == 2) {  // (the runtime's stream wait needs device support)
         int wv = 0;
-        e->gate_ = env_int("JPGE_GATE", 1, 0, 1) != 0 &&
-                   hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv;
+        if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess || !wv) e->gate_ = 0;
         (void)hipGetLastError();
     }
     e->hist_nap_us_ = env_int("JPGE_HIST_NAP_US", e->hist_nap_us_, 0, 1000);
@@ -1066,7 +1066,7 @@ int Encoder::launch_entropy_phase(Slot& s, Slot* exp, bool lone, int parts) {
     // instead (write-through cost it 1.3%) and awaits its stream at the batch's end.
     if (lone && lanes_.size() == 1)
         e.pack_done = reinterpret_cast<uint32_t*>(s.d_ctl + CtlLayout(slot_layout(s).grid()).done + kPackDoneOff);
-    s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1)
+    if (parts == 3) s.h_result[2] = 0;  // (the slot's previous entropy kernel finished before phase1; gated: encode())
     e.exp_hist = exp ? exp->hist : HistPtrs{};
     e.exp_cnt = exp ? exp->d_hist_host->cnt : nullptr;
     e.exp_key = exp ? exp->d_hist_host->key : nullptr;
@@ -1149,9 +1149,20 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
         }
         ~Gate() { open(); }
     } gate{s.gate(), (uint32_t)s.seq};
-    if (!st && gate_) {
+    if (!st && gate_ == 1) {  // a workgroup of ours waits and copies (entropy.hip gate_copy_kernel)
+        s.h_result[2] = 0;  // (its time-out flag)
+        if (launch_gate_copy(reinterpret_cast<const uint32_t*>(s.d_result_host + 6), gate.value, s.d_tab_host, s.d_tab,
+                             (uint32_t)((kTabBytes + kHdrMax) / 16), s.d_result_host + 2, s.stream) == hipSuccess) {
+            gate.shut = true;
+            st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/1);
+            if (st) gate.open();
+        } else {
+            st = kErrHip;
+        }
+    } else if (!st && gate_ == 2) {  // the runtime's stream wait, then a copy
         if (hipStreamWaitValue32(s.stream, gate.word, gate.value, hipStreamWaitValueEq, 0xFFFFFFFFu) == hipSuccess) {
             gate.shut = true;
+            s.h_result[2] = 0;
             if (hipMemcpyAsync(s.d_tab, s.h_tab, kTabBytes + kHdrMax, hipMemcpyHostToDevice, s.stream) != hipSuccess)
                 st = kErrHip;
             if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/1);

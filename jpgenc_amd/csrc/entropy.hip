@@ -875,6 +875,43 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
     return L;
 }
 
+// encode()'s gate (encoder.cpp): one workgroup waits for the host's word, then copies the
+// tables and headers from mapped host memory to the device, ahead of the code kernel.  A
+// time-out (~1 s) ends the wait whatever happens and flags the frame's result word
+// (host_result[2]), so the call fails instead of coding with stale tables.
+constexpr uint32_t kGateThreads = 512;
+constexpr uint64_t kGateTimeoutTicks = 100000000ull;  // s_memrealtime runs at 100 MHz
+__global__ __launch_bounds__(kGateThreads) void gate_copy_kernel(const uint32_t* gate, uint32_t value, const uint4* src,
+                                                                 uint4* dst, uint32_t n16, uint64_t* fail) {
+    __shared__ uint32_t open;
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t o = 1;
+        while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
+            __builtin_amdgcn_s_sleep(4);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+                o = 0;
+                break;
+            }
+        }
+        open = o;
+    }
+    __syncthreads();
+    if (!open) {
+        if (threadIdx.x == 0) __hip_atomic_store(fail, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // (the host's table stores precede its word)
+    for (uint32_t i = threadIdx.x; i < n16; i += kGateThreads) dst[i] = src[i];
+}
+
+hipError_t launch_gate_copy(const uint32_t* gate, uint32_t value, const void* src, void* dst, uint32_t n16,
+                            uint64_t* fail, hipStream_t s) {
+    hipLaunchKernelGGL(gate_copy_kernel, dim3(1), dim3(kGateThreads), 0, s, gate, value,
+                       reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16, fail);
+    return hipGetLastError();
+}
+
 hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tcode, const KTimer* tpack) {
     const hipError_t e = launch_entropy_code(a, s, tcode);
     return e != hipSuccess ? e : launch_entropy_pack(a, s, tpack);

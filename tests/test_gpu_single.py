@@ -9,7 +9,8 @@ compared with the oracle; host output and a frame too big for its buffer as well
 The tables' copy and the code kernel wait behind a stream gate the host opens once the
 tables are built (encode()'s gate); a call that fails after queueing them (the header
 does not fit the buffer) must still open it, and the context must keep working.  With
-JPGE_GATE=0 the same bytes come from the ungated launches."""
+JPGE_GATE=0 (no gate) and 2 (the runtime's stream wait and copy instead of the library's
+wait-and-copy workgroup) the same bytes come out."""
 import numpy as np
 import pytest
 
@@ -71,8 +72,9 @@ def test_header_does_not_fit(lone):
     assert big[:n].cpu().numpy().tobytes() == _oracle.encode(rgb, 90)
 
 
-def test_gate_off_same_bytes(monkeypatch):
-    monkeypatch.setenv("JPGE_GATE", "0")
+@pytest.mark.parametrize("mode", ["0", "2"])  # no gate; the runtime's stream wait
+def test_gate_modes_same_bytes(monkeypatch, mode):
+    monkeypatch.setenv("JPGE_GATE", mode)
     enc = J.Encoder(0, lanes=1)
     try:
         for w, h, q in [(1920, 1080, 90), (200, 136, 50)]:
