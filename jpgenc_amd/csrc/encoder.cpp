@@ -1141,17 +1141,17 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     // reads the tables h_tab holds, valid ones or zeros, and its output is discarded.)
     struct Gate {  // (opened at the latest when the call unwinds)
         uint32_t* word;
-        uint32_t value;  // (the frame's sequence number: differs from the previous call's)
+        uint32_t value;  // (the word holds the previous gated call's value, one less)
         bool shut = false;
         void open() {
             if (shut) __atomic_store_n(word, value, __ATOMIC_RELEASE);
             shut = false;
         }
         ~Gate() { open(); }
-    } gate{s.gate(), (uint32_t)s.seq};
+    } gate{s.gate(), gate_count_ + 1};
+    if (!st && gate_) ++gate_count_;
     if (!st && gate_ == 1) {  // a workgroup of ours waits and copies (entropy.hip gate_copy_kernel)
         s.h_result[2] = 0;  // (its time-out flag)
-        __atomic_store_n(gate.word, ~gate.value, __ATOMIC_RELAXED);  // (shut whatever the word held)
         if (launch_gate_copy(reinterpret_cast<const uint32_t*>(s.d_result_host + 6), gate.value, s.d_tab_host, s.d_tab,
                              (uint32_t)((kTabBytes + kHdrMax) / 16), s.d_result_host + 2, s.stream) == hipSuccess) {
             gate.shut = true;
@@ -1161,7 +1161,6 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
             st = kErrHip;
         }
     } else if (!st && gate_ == 2) {  // the runtime's stream wait, then a copy
-        __atomic_store_n(gate.word, ~gate.value, __ATOMIC_RELAXED);
         if (hipStreamWaitValue32(s.stream, gate.word, gate.value, hipStreamWaitValueEq, 0xFFFFFFFFu) == hipSuccess) {
             gate.shut = true;
             s.h_result[2] = 0;

@@ -172,6 +172,7 @@ class Encoder {
     std::unique_ptr<TableHelper> helper_;  // single images on a 1-lane encoder: a second table thread
     bool table_helper_ = true;             // JPGE_TABLE_HELPER=0: none
     int gate_ = 1;  // encode()'s gate: 1 our wait-and-copy kernel, 2 the runtime's stream wait (JPGE_GATE), 0 none
+    uint32_t gate_count_ = 0;  // gated calls (their gate values: 1, 2, ...)
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
