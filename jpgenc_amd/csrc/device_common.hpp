@@ -65,6 +65,12 @@ static __constant__ uint8_t kNatToZz[64] = {
     10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
+// zig-zag position -> natural index (Coding.hpp:57-81)
+static __constant__ uint8_t kZzToNat[64] = {
+    0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
 // Orders LDS traffic between lanes of ONE wavefront (a wave's DS ops execute in
 // order; this stops the compiler from moving them across the point).
 __device__ __forceinline__ void wave_lds_sync() {

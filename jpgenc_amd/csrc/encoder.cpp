@@ -10,7 +10,6 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
-#include <deque>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -164,9 +163,7 @@ inline int wait_seq(const uint64_t* word, uint64_t seq, hipStream_t stream, int 
 // Pipeline depth limits (defaults in Encoder; the slots in flight = lookahead + drain lag + 1).
 constexpr int kMaxLookahead = 8;
 constexpr int kMaxDrainLag = 4;
-constexpr int kMaxTableThreads = 16;
 constexpr int kMaxLanes = 8;
-constexpr uint64_t kInlineTablesMinPixels = 4u << 20;  // frames this large build their tables on the lane thread
 constexpr uint64_t kFirstSleepMaxPixels = 16u << 20;   // frames this large poll their results without a first sleep
 
 double abs_us(std::chrono::steady_clock::time_point t) {  // host-trace clock
@@ -210,101 +207,6 @@ struct HostHist {  // written by hist_export_kernel into mapped pinned memory
 };
 
 }  // namespace
-
-// Host worker threads for the Huffman-table build (package-merge with libstdc++
-// heap order is inherently serial per table, so frames are built side by side).  A
-// job carries a readiness test (its histograms have arrived): workers take any ready
-// job, so a frame whose histograms are still queued on the GPU never holds up one
-// whose histograms are in (with several lanes, jobs finish out of order).
-class Encoder::TablePool {
-  public:
-    using clk = std::chrono::steady_clock;
-    struct Job {
-        std::function<bool()> ready;
-        std::function<void()> run;
-        clk::time_point submit;
-    };
-    explicit TablePool(int n, double first_sleep) : frac_(first_sleep) {
-        for (int i = 0; i < n; ++i)
-            th_.emplace_back([this, i] {
-                prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // ~1 us sleeps while polling
-                const std::string name = "jpge-tab" + std::to_string(i);
-                prctl(PR_SET_NAME, name.c_str(), 0, 0, 0);
-                loop();
-            });
-    }
-    ~TablePool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    void submit(Job job) {
-        job.submit = clk::now();
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            q_.push_back(std::move(job));
-        }
-        cv_.notify_one();
-    }
-
-  private:
-    // One worker at a time polls for a ready job (the others wait on the condition
-    // variable): it sleeps until the earliest job is likely ready (its submit time plus
-    // frac_ of the usual submit-to-ready delay), then naps ~10 us between looks.  (Every
-    // worker napping on its own cost ~0.8 CPU per worker with 1080p frames.)
-    void loop() {
-        std::unique_lock<std::mutex> lk(mu_);
-        for (;;) {
-            if (q_.empty()) {
-                if (stop_) return;
-                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
-                continue;
-            }
-            const auto now = clk::now();
-            auto it = std::find_if(q_.begin(), q_.end(), [](const Job& j) { return j.ready(); });
-            if (it != q_.end()) {
-                const double us = std::chrono::duration<double, std::micro>(now - it->submit).count();
-                if (ready_us_ > 0) ready_dev_ = 0.85 * ready_dev_ + 0.15 * std::fabs(us - ready_us_);
-                ready_us_ = ready_us_ > 0 ? 0.85 * ready_us_ + 0.15 * us : us;
-                std::function<void()> run = std::move(it->run);
-                q_.erase(it);
-                if (!q_.empty()) cv_.notify_one();  // (someone polls for the rest)
-                lk.unlock();
-                run();
-                lk.lock();
-                continue;
-            }
-            if (polling_) {  // another worker polls
-                cv_.wait(lk);
-                continue;
-            }
-            polling_ = true;
-            auto wake = now + std::chrono::microseconds(10);
-            if (frac_ > 0 && ready_us_ > 0) {
-                auto first = q_.front().submit;
-                for (const Job& j : q_) first = std::min(first, j.submit);
-                const auto due = first + std::chrono::microseconds((long)(frac_ * ready_us_ - 2.0 * ready_dev_));
-                if (due > wake) wake = due;
-            }
-            lk.unlock();
-            std::this_thread::sleep_until(wake);
-            lk.lock();
-            polling_ = false;
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Job> q_;
-    bool stop_ = false;
-    bool polling_ = false;
-    double frac_ = 0;      // first sleep, of the usual submit-to-ready delay
-    double ready_us_ = 0;  // smoothed submit-to-ready delay of the jobs (upper bound: when first seen ready)
-    double ready_dev_ = 0;  // smoothed |delay - ready_us_|
-};
 
 // A 1-lane encoder's second table thread, for single images (encode()): while the calling
 // thread builds the luma AC table (the largest: ~2/3 of a frame's table time), it builds
@@ -436,7 +338,7 @@ struct Encoder::Slot {
     uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
     uint32_t img_w = 0, img_h = 0;
     int tables_status = 0;
-    bool inline_tables = false;  // this frame's tables are built by its lane's thread (else the pool)
+    bool inline_tables = false;  // this frame's tables are built inside its lane's pipeline (its waits use the lane's guess)
     // the lane's wait estimates (histograms when its own thread builds the tables; results)
     WaitGuess* guess_hist = nullptr;
     WaitGuess* guess_result = nullptr;
@@ -564,16 +466,12 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->lookahead_ = env_int("JPGE_LOOKAHEAD", e->lookahead_, 1, kMaxLookahead);
     e->drain_lag_ = env_int("JPGE_DRAIN_LAG", e->drain_lag_, 0, kMaxDrainLag);
     e->set_ = env_int("JPGE_SET", 0, 0, kMaxSet);
-    e->table_threads_ = env_int("JPGE_TABLE_THREADS", e->table_threads_, 1, kMaxTableThreads);
-    e->inline_tables_ = env_int("JPGE_INLINE_TABLES", e->inline_tables_, 0, 3);
     e->nap_us_ = env_int("JPGE_NAP_US", e->nap_us_, 1, 1000);
     e->first_sleep_ = env_int("JPGE_FIRST_SLEEP", (int)(e->first_sleep_ * 100 + 0.5), 0, 95) / 100.0;
-    // (the table pool sleeps first only when asked: the 1080p batch lost 9% to it)
-    e->pool_first_sleep_ = std::getenv("JPGE_FIRST_SLEEP") ? e->first_sleep_ : 0.0;
     const int nap = env_int("JPGE_NAP", -1, -1, 1);
-    e->end_sync_ = env_int("JPGE_END_SYNC", e->end_sync_, 0, 2);
     e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
     e->place_in_code_ = env_int("JPGE_PLACE_IN_CODE", 1, 0, 1) != 0;
+    e->coef_code_ = env_int("JPGE_CODE_COEF", 0, 0, 1) != 0;
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -682,7 +580,6 @@ Encoder::~Encoder() {
     helper_.reset();
     for (auto& ln : lanes_) ln->shutdown();
     for (auto& b : scratch_) hipFree(b.first);
-    pool_.reset();  // (no jobs are pending between calls)
     hipSetDevice(device_);
     for (auto& ln : lanes_) {
         if (ln->stream) hipStreamSynchronize(ln->stream);
@@ -721,7 +618,7 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     const CtlLayout L(layout(g).grid());
     const size_t ntiles = seg_tiles(layout(g));
     const size_t nrecs = (size_t)seg_tiles(layout(g)) * kTileRecords;
-    if (ntiles > s.cap_tiles || nrecs > s.cap_recs) {
+    if (!coef_code_ && (ntiles > s.cap_tiles || nrecs > s.cap_recs)) {
         hipFree(s.d_recs); hipFree(s.d_tcount);
         s.d_recs = nullptr; s.d_tcount = nullptr; s.cap_tiles = s.cap_recs = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_recs, nrecs * sizeof(*s.d_recs)));
@@ -794,8 +691,8 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.key_c0 = s.key_c0;
     st.key_ncb = s.key_ncb;
     st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs());
-    st.recs = s.d_recs;
-    st.tcount = s.d_tcount;
+    st.recs = coef_code_ ? nullptr : s.d_recs;
+    st.tcount = coef_code_ ? nullptr : s.d_tcount;
     st.wgs = stats_wgs();
     if (!stats_wgs_ && lanes_.size() > 1) {
         // frames under ~3 MPix (fewer than 3 tiles per workgroup at 384): about 3 tiles per
@@ -812,8 +709,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     const CtlLayout L(slot_layout(s).grid());
     EntropyArgs e;
     e.coef = s.d_coef;
-    e.recs = s.d_recs;
-    e.tcount = s.d_tcount;
+    e.recs = coef_code_ ? nullptr : s.d_recs;
+    e.tcount = coef_code_ ? nullptr : s.d_tcount;
     e.g = s.g;
     e.tables = s.d_tab;
     e.out = s.out_dev;
@@ -964,7 +861,7 @@ int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a_in, const Stats
     return kOk;
 }
 
-// Phase 2a (host; the calling thread or a pool worker): wait for the histograms,
+// Phase 2a (host; the calling thread or a lane's thread): wait for the histograms,
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel, TableHelper* helper) {
@@ -1201,12 +1098,12 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     // it; ~9 us).  Host
     // output: the copy queued by finish(), awaited by spinning as a batch lane's end (a
     // blocking stream synchronisation adds tens of us of wake-up).
-    const bool await_end = st || !(flags & kFlagDeviceOutput) || end_sync_ != 0 || lanes_.size() != 1;
+    const bool await_end = st || !(flags & kFlagDeviceOutput) || lanes_.size() != 1;
     if (await_end) {
-        if (end_sync_ == 2 || hipEventRecord(lanes_[0]->done, s.stream) != hipSuccess) {
+        if (hipEventRecord(lanes_[0]->done, s.stream) != hipSuccess) {
             hipStreamSynchronize(s.stream);
         } else {
-            const hipError_t w = end_sync_ == 1 ? hipEventSynchronize(lanes_[0]->done) : wait_event(lanes_[0]->done);
+            const hipError_t w = wait_event(lanes_[0]->done);
             if (w != hipSuccess && !st) st = kErrHip;
         }
     }
@@ -1233,8 +1130,6 @@ int Encoder::encode_batch(FrameDesc* fr, int n, const uint8_t qy[64], const uint
     JPGE_HIP(hipSetDevice(device_));
     for (int i = 0; i < n; ++i) fr[i].status = 0;
     if (n <= 0) return kOk;
-    if ((inline_tables_ == 0 || inline_tables_ == 2) && !pool_ && n > 1)
-        pool_.reset(new TablePool(table_threads_, pool_first_sleep_));
     // Frames are dealt dynamically: a lane takes the batch's next frame (or frame set)
     // when its pipeline has room, so lanes finish together.  Lane 0 runs on the calling
     // thread.
@@ -1322,9 +1217,10 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
     // member m of the other for the carried duties.  The pipeline's edges fall back to a
     // standalone export kernel and a table copy.
     const int L = lookahead_, D = drain_lag_;
-    // (JPGE_INLINE_TABLES=3) this lane's frames whose tables are not built yet; the
-    // lane's waits build any whose histograms are in (the ~25 us of a 1080p frame's
-    // tables fill a wait instead of a pool worker's polling and hand-off)
+    // This lane's frames whose tables are not built yet: the lane's waits build any whose
+    // histograms are in (the ~25 us of a 1080p frame's tables fill a wait instead of a
+    // worker's polling and hand-off), and a frame's entropy launch builds its own if they
+    // are still missing.
     std::vector<Slot*> pend;
     pend.reserve((size_t)(L + D + 2) * set);
     const std::function<bool()> build_ready = [&]() -> bool {
@@ -1343,36 +1239,9 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
         return false;
     };
     auto submit_tables = [&](Slot& s) {
-        // Large frames: built by this lane's thread when the frame's entropy launch needs
-        // them (below): no pool workers polling for histograms, no hand-off (4K: the same
-        // throughput at 2.6 instead of 3.5 CPUs).  Small frames come several times as
-        // often per lane; their tables go to the pool, whose workers build them beside
-        // the lane threads (1080p batch: 90.2 vs 82.5 GPix/s).
-        s.inline_tables = inline_tables_ == 1 || inline_tables_ == 3 ||
-                          (inline_tables_ == 2 && (uint64_t)s.g.width * s.g.height >= kInlineTablesMinPixels) || !pool_;
-        if (s.inline_tables) {
-            s.tables_done.store(0, std::memory_order_relaxed);
-            if (inline_tables_ == 3) pend.push_back(&s);
-        } else if (pool_) {
-            Slot* sp = &s;
-            const int dev = device_;
-            // ready once the histograms are in (or after 2 ms, when build_tables'
-            // own bounded wait takes over and reports a failed stream)
-            sp->t_submit = std::chrono::steady_clock::now();
-            const auto due = sp->t_submit + std::chrono::milliseconds(2);
-            pool_->submit({[sp, due] {
-                               return __atomic_load_n(&sp->h_hist->seq, __ATOMIC_ACQUIRE) == sp->seq ||
-                                      std::chrono::steady_clock::now() > due;
-                           },
-                           [this, sp, dev] {
-                               sp->t_start = std::chrono::steady_clock::now();
-                               hipSetDevice(dev);
-                               sp->tables_status = build_tables(*sp, false);
-                               sp->t_done = std::chrono::steady_clock::now();
-                               sp->tables_done.store(1, std::memory_order_release);
-                           },
-                           {}});
-        }
+        s.tables_done.store(0, std::memory_order_relaxed);
+        s.inline_tables = true;
+        pend.push_back(&s);
     };
     // diagnostic host trace: (step, point, us since the call, and at point 1 the
     // awaited table job's submit / start / done times)
@@ -1421,13 +1290,9 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
             for (int m = 0; m < members(j); ++m) {
                 if (frame(j, m).status) continue;
                 Slot& s = slot(j, m);
-                if (s.inline_tables && !s.tables_done.load(std::memory_order_acquire)) {
+                if (!s.tables_done.load(std::memory_order_acquire)) {
                     s.tables_status = build_tables(s, /*parallel=*/false);
                     s.tables_done.store(1, std::memory_order_release);
-                }
-                while (!s.tables_done.load(std::memory_order_acquire)) {
-                    if (nap_) std::this_thread::sleep_for(std::chrono::microseconds(nap_us_));
-                    else std::this_thread::yield();
                 }
                 if (s.tables_status) note(j, m, s.tables_status);
                 else sj[m] = &s;
@@ -1559,13 +1424,8 @@ int Encoder::run_lane(Lane& ln, FrameDesc* frames, int total, std::atomic<int>* 
     }
     // every output byte is in place: the stream's tail, awaited by spinning (a
     // blocking stream synchronisation adds tens of us of wake-up latency)
-    if (end_sync_ == 2) {
-        JPGE_HIP(hipStreamSynchronize(ln.stream));
-    } else {
-        JPGE_HIP(hipEventRecord(ln.done, ln.stream));
-        if (end_sync_ == 1) JPGE_HIP(hipEventSynchronize(ln.done));
-        else JPGE_HIP(wait_event(ln.done));
-    }
+    JPGE_HIP(hipEventRecord(ln.done, ln.stream));
+    JPGE_HIP(wait_event(ln.done));
     mark(n + L + D, 5);  // (n: this lane's set count)
     if (cpu_prof_) {
         for (int q = 0; q < 6; ++q) cpu_ns_[q].fetch_add(cpu_acc[q], std::memory_order_relaxed);

@@ -126,7 +126,6 @@ class Encoder {
   private:
     struct Slot;
     struct Lane;
-    class TablePool;
     class TableHelper;
     Encoder() = default;
     int ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap);
@@ -168,7 +167,6 @@ class Encoder {
     int timing_every_ = 0;
     std::atomic<uint64_t> frame_counter_{0};
     std::atomic<uint64_t> seq_counter_{0};
-    std::unique_ptr<TablePool> pool_;
     std::unique_ptr<TableHelper> helper_;  // single images on a 1-lane encoder: a second table thread
     bool table_helper_ = true;             // JPGE_TABLE_HELPER=0: none
     int gate_ = 1;  // encode()'s gate: 1 our wait-and-copy kernel, 2 the runtime's stream wait (JPGE_GATE), 0 none
@@ -194,25 +192,18 @@ class Encoder {
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain
     int set_ = 0;               // JPGE_SET: frames per launch (0: batch_set_size decides)
-    int table_threads_ = 4;     // JPGE_TABLE_THREADS: host workers building Huffman tables (JPGE_INLINE_TABLES=0)
-    // JPGE_INLINE_TABLES: who builds a frame's Huffman tables.  3 (default): its lane's
-    // thread, as soon as the histograms are in, inside the waits of its pipeline (or when
-    // the entropy launch needs them); 1: its lane's thread when the entropy launch needs
-    // them; 0: the table pool; 2: by frame size (encoder.cpp kInlineTablesMinPixels).
-    int inline_tables_ = 3;
     int nap_us_ = 40;           // JPGE_NAP_US: a napping thread's sleep between polls (10: equal throughput, more wake-ups)
     // JPGE_FIRST_SLEEP (percent): a lane's first sleep in a result wait, of its usual length
     // less twice its spread (WaitGuess).  At 80%: 4K host CPU 1.45 -> 1.22 at equal
     // throughput; frames above kFirstSleepMaxPixels (16384^2: -3.7%) poll without it.
     double first_sleep_ = 0.8;
-    double pool_first_sleep_ = 0;  // the table pool's (JPGE_FIRST_SLEEP given: the same)
     // JPGE_EXT_PLACE: 1 = entropy placement by the scan kernel at every size, 0 = by each
     // pack workgroup up to kInlineScanMaxWgs; default (-1): the scan kernel beside other
     // lanes (one small launch instead of every pack workgroup scanning all records:
     // +0.8% in the pipeline), inline alone (one launch less per frame)
     int ext_place_ = -1;
     bool place_in_code_ = true;  // JPGE_PLACE_IN_CODE: the last code workgroup places (pipeline)
-    int end_sync_ = 0;          // JPGE_END_SYNC: batch end by 0 event polling, 1 event sync, 2 stream sync
+    bool coef_code_ = false;     // JPGE_CODE_COEF: the code kernel reads coefficients (else K2's symbol records)
     bool nap_ = false;          // lane threads sleep ~10 us between polls instead of spinning (default: >1 lane; JPGE_NAP)
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
     bool cpu_prof_ = false;                  // JPGE_CPU_PROF: lane threads' CPU per loop segment (printed at close)

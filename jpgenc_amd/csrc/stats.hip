@@ -72,12 +72,6 @@ static_assert(kWCopies <= 32 && kWCopyWords % 32 == kWBankStep && kWCopyWords >=
 constexpr uint32_t kWKeyWords = (kWSyms + 1 + 3) / 4 * 4;  // keys, then one shared dummy word
 constexpr uint32_t kWMaxSubs = 1024;  // sub-streams per workgroup, at most (stats_grid)
 
-// zig-zag position -> natural index (inverse of Coding.hpp:57-81)
-static __constant__ uint8_t kZzToNat[64] = {
-    0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
-    41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
-    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-
 struct K2WLds {
     alignas(16) uint32_t stage[kWWaves][8 * 32 + 32];   // each wave's 8-block chunk: int16 [block][64], natural order; 64 spare int16
     alignas(16) uint32_t cnt[kWCopies * kWCopyWords];    // counters [copy][word], then the dummies
@@ -86,7 +80,9 @@ struct K2WLds {
     uint32_t next;                                       // the next sub-stream to take
 };
 
-template <int kN>
+// kRecs: also write the symbol records (the record-reading code kernel); without them
+// (a.recs == nullptr) the code kernel re-derives the symbols from the coefficients.
+template <int kN, bool kRecs>
 __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe))) void stats_wave_kernel(FrameSet<StatsArgs, kN> fs) {
     const uint32_t set_f = (kN == 1 ? 0u : set_member_rolled(fs.wg0, fs.n, blockIdx.x));  // (frame sets: kernels.hpp)
     const StatsArgs& a = fs.a[set_f];
@@ -277,7 +273,8 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 b.rk += zi;
                 if (nzr) {
                     const uint32_t zrec = b.Tj | (0xF0u << 16);
-                    for (uint32_t z = 1; z <= nzr; ++z) srec[base + b.rk - z] = zrec;
+                    if constexpr (kRecs)
+                        for (uint32_t z = 1; z <= nzr; ++z) srec[base + b.rk - z] = zrec;
                     const uint32_t wz = b.acw + kRunStride * 15u;  // (symbol 0xF0)
                     atomicAdd(&cnt[wz], nzr);
                     const uint32_t kz = b.acbj + k2p - 1u;
@@ -285,7 +282,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 }
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b.em)) {
-                srec[base + b.rk] = b.rec;
+                if constexpr (kRecs) srec[base + b.rk] = b.rec;
                 atomicAdd(&cnt[b.w], 1u);
                 const uint32_t kk = b.acbj + k2p;
                 if (kk < L.key[b.w]) atomicMin(&L.key[b.w], kk);
@@ -317,8 +314,10 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                     // are masked off
                     baseB = base + (uint32_t)__builtin_popcountll(A.em);
                     const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
-                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
+                    if constexpr (kRecs) {
+                        __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
+                    }
                     if (ia) atomicAdd(&cnt[A.w], 1u);
                     if (ib) atomicAdd(&cnt[B.w], 1u);
                     // (every lane reads its word: a lane without a record has c = 0, so its
@@ -342,7 +341,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             if (jb < j1) base += emit(cp[0], jb, base);  // an odd last block
         }
         JPGE_ACC(2, tq);
-        if (lane == 0) a.tcount[s] = base;
+        if (kRecs && lane == 0) a.tcount[s] = base;
         si = sn;
         JPGE_ACC(3, tq);
     }
@@ -411,7 +410,8 @@ static hipError_t launch_stats_fs(const FrameSet<StatsArgs, kN>& fs, hipStream_t
         if ((uint64_t)fs.a[f].g.nblocks() * 128 >= (1ull << 32)) return hipErrorInvalidValue;
         if (fs.wg0[f + 1] - fs.wg0[f] != stats_grid(fs.a[f].seg, fs.a[f].wgs)) return hipErrorInvalidValue;
     }
-    return launch_timed(t, stats_wave_kernel<kN>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
+    if (fs.a[0].recs) return launch_timed(t, stats_wave_kernel<kN, true>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
+    return launch_timed(t, stats_wave_kernel<kN, false>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
