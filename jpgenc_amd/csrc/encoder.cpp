@@ -471,7 +471,6 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     const int nap = env_int("JPGE_NAP", -1, -1, 1);
     e->ext_place_ = env_int("JPGE_EXT_PLACE", -1, -1, 1);
     e->place_in_code_ = env_int("JPGE_PLACE_IN_CODE", 1, 0, 1) != 0;
-    e->coef_code_ = env_int("JPGE_CODE_COEF", 0, 0, 1) != 0;
     if (e->stamps_file_) {
         e->dbg_words_ = 4ull * 65536 * kStampSlots;  // up to 64k workgroups per kernel, 4 kernels
         JPGE_HIP(hipMalloc((void**)&e->d_dbg_, e->dbg_words_ * 8));
@@ -618,7 +617,7 @@ int Encoder::ensure(Slot& s, const Geometry& g, size_t in_bytes, size_t out_cap)
     const CtlLayout L(layout(g).grid());
     const size_t ntiles = seg_tiles(layout(g));
     const size_t nrecs = (size_t)seg_tiles(layout(g)) * kTileRecords;
-    if (!coef_code_ && (ntiles > s.cap_tiles || nrecs > s.cap_recs)) {
+    if (ntiles > s.cap_tiles || nrecs > s.cap_recs) {
         hipFree(s.d_recs); hipFree(s.d_tcount);
         s.d_recs = nullptr; s.d_tcount = nullptr; s.cap_tiles = s.cap_recs = 0;
         JPGE_HIP(hipMalloc((void**)&s.d_recs, nrecs * sizeof(*s.d_recs)));
@@ -691,8 +690,8 @@ StatsArgs Encoder::stats_args(Slot& s) {
     st.key_c0 = s.key_c0;
     st.key_ncb = s.key_ncb;
     st.seg = seg_layout(s.g, s.rst.mcus, entropy_wgs());
-    st.recs = coef_code_ ? nullptr : s.d_recs;
-    st.tcount = coef_code_ ? nullptr : s.d_tcount;
+    st.recs = s.d_recs;
+    st.tcount = s.d_tcount;
     st.wgs = stats_wgs();
     if (!stats_wgs_ && lanes_.size() > 1) {
         // frames under ~3 MPix (fewer than 3 tiles per workgroup at 384): about 3 tiles per
@@ -709,8 +708,8 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     const CtlLayout L(slot_layout(s).grid());
     EntropyArgs e;
     e.coef = s.d_coef;
-    e.recs = coef_code_ ? nullptr : s.d_recs;
-    e.tcount = coef_code_ ? nullptr : s.d_tcount;
+    e.recs = s.d_recs;
+    e.tcount = s.d_tcount;
     e.g = s.g;
     e.tables = s.d_tab;
     e.out = s.out_dev;

@@ -203,7 +203,6 @@ class Encoder {
     // +0.8% in the pipeline), inline alone (one launch less per frame)
     int ext_place_ = -1;
     bool place_in_code_ = true;  // JPGE_PLACE_IN_CODE: the last code workgroup places (pipeline)
-    bool coef_code_ = false;     // JPGE_CODE_COEF: the code kernel reads coefficients (else K2's symbol records)
     bool nap_ = false;          // lane threads sleep ~10 us between polls instead of spinning (default: >1 lane; JPGE_NAP)
     const char* host_trace_file_ = nullptr;  // JPGE_HOST_TRACE: append per-iteration host timestamps
     bool cpu_prof_ = false;                  // JPGE_CPU_PROF: lane threads' CPU per loop segment (printed at close)

@@ -380,259 +380,6 @@ __device__ void write_wg_record(const EntropyArgs& a, uint32_t wg, uint32_t G, c
     }
 }
 
-// ---------------------------------------------------------------------------
-// entropy_coef_kernel: the code kernel without symbol records.  It reads the int16
-// coefficients K1 wrote (24.9 MB per 4K frame) instead of K2's 4-byte records
-// (28.9 MB written by K2 and read back here at Q90, 44 MB at Q100), re-deriving each
-// block's symbols the way K2 counted them: same partition, same workgroup streams,
-// same WgRecord, so placement and the pack kernel are unchanged.
-//
-// Rounds of kCRound blocks: wave w codes the round's w-th chunk of 8 consecutive
-// blocks, one wave per block at a time (lane p = zig-zag position p, as in K2):
-//   c = the coefficient at zig-zag position p (lane 0: the block's DC difference)
-//   M = ballot(c != 0) without the DC; run = zeros since the previous non-zero;
-//   cat = bit length of |c|; the symbol's code from the LDS table, then the extra
-//   bits (Coding.hpp:197-230, Image.cpp:737-829); lane 63 codes the EOB when
-//   coefficient 63 is zero; a run of 16+ zeros puts ZRL codes ahead of its symbol
-// A wave scan of the lanes' bit counts gives every string's offset inside the
-// chunk; the strings wait in registers (two words per lane and block) until one
-// workgroup scan of the chunks' totals places the chunks in the round, then each
-// lane ORs its string into the workgroup's big-endian stage (at most two words).
-// The stage is flushed to the workgroup's region as before (complete words, 0xFF
-// counts at the 8 alignments), when the round would not fit and at the end.
-constexpr int kCWaves = kK3Waves;       // 8
-constexpr int kCChunk = 8;              // blocks per wave and round
-constexpr int kCRound = kCWaves * kCChunk;  // 64 blocks per round
-constexpr int kCBlockBits = 1665;       // a block's worst case (kStageBytesPerBlock)
-constexpr int kCStageWords = (kCRound * kCBlockBits + 31) / 32 + 6;  // a worst-case round + carry, multiple of 4
-static_assert(kCStageWords % 4 == 0, "the stage zeroes in 16-byte stores");
-constexpr uint32_t kCStageBits = (kCStageWords - 2) * 32;
-static_assert(kCStageBits >= (uint32_t)kCRound * kCBlockBits + 31, "a round fits the stage after a flush");
-
-struct KCLds {
-    uint32_t stage[kCStageWords];                  // offset 0: 16-byte aligned
-    uint32_t tab[4 * 256];                         // lds_tab_entry
-    alignas(16) uint32_t cst[kCWaves][8 * 32 + 32];  // each wave's chunk: int16 [block][64] natural order; 64 spare int16
-    alignas(8) uint32_t wtot[2][kCWaves];          // chunk totals of the rounds, alternating (place_all's scans)
-    uint32_t cnt8[8];
-    uint32_t carry;
-};
-
-template <int kN>
-__global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3Wpe))) void entropy_coef_kernel(
-    FrameSet<EntropyArgs, kN> fs) {
-    __shared__ KCLds L;
-    const uint32_t set_f = set_member<kN>(fs.wg0, fs.n, blockIdx.x);  // (frame sets: kernels.hpp)
-    const EntropyArgs& a = fs.a[set_f];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t wg = blockIdx.x - fs.wg0[set_f], G = fs.wg0[set_f + 1] - fs.wg0[set_f];
-    JPGE_STAMP(0);
-    if (a.exp_cnt && wg == 0)  // carried: a later frame's histograms to the host
-        export_hist<kK3Threads>(a.exp_hist, a.exp_cnt, a.exp_key, a.exp_seq, a.exp_seqv, tid);
-    if (tid == 0) L.carry = 0;
-    if (tid < 8) L.cnt8[tid] = 0;
-    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = lds_tab_entry(a.tables[i], (uint32_t)i);
-    for (int i = tid; i < kCStageWords / 4; i += kK3Threads) reinterpret_cast<uint4*>(L.stage)[i] = make_uint4(0, 0, 0, 0);
-    const WgTiles wt = wg_tiles(a.seg, wg);  // 1..kMaxTiles tiles of one segment (seg_layout)
-    const uint32_t B0 = (uint32_t)wt.tile_b0(wt.t0);  // the workgroup's blocks [B0, B0 + nblk) (< 2^25: launch)
-    const uint32_t nblk = (uint32_t)wt.tile_b0(wt.t0 + wt.nt) - B0;
-    const uint32_t nrounds = (nblk + kCRound - 1) / kCRound;
-    uint8_t* R8 = a.ubuf + (uint64_t)wg * kEntropyRegionBytes;
-    uint32_t* R32 = reinterpret_cast<uint32_t*>(R8);
-
-    const uint32_t bpm = a.g.bpm, nfb = a.g.nblocks();
-    const uint32_t natoff = kZzToNat[lane];
-    const uint32_t shl = (uint32_t)(64 - lane) & 63u;
-    const uint32_t tdc = lane == 0 ? 0u : 256u;  // lane 0 codes the DC (tables 0 / 2), the others AC (1 / 3)
-    int16_t* st16 = reinterpret_cast<int16_t*>(L.cst[wv]);
-    uint4* st4 = reinterpret_cast<uint4*>(L.cst[wv]);
-    // the workgroup's coefficients (zeros past its blocks) and the chunks' DC predecessors
-    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int16_t*>(a.coef + (uint64_t)B0 * 64), 0, nblk * 128, 0x00020000);
-    auto load_chunk = [&](uint32_t ci) {
-        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(crs, ci * (kCChunk * 128u) + (uint32_t)lane * 16u, 0, 0));
-    };
-    auto load_dc = [&](uint32_t ci) -> int {  // lane l < 14: the DC of block c0 - 6 + l
-        const int32_t g = (int32_t)(B0 + ci * kCChunk + (uint32_t)lane) - 6;
-        return (lane < kCChunk + 6 && g >= 0 && (uint32_t)g < nfb) ? a.coef[(uint64_t)(uint32_t)g * 64] : 0;
-    };
-
-    uint32_t c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    auto count_word = [&](uint32_t x, uint32_t nx) {
-        uint32_t y = x;  // bit 31-t: stream bits [32m+t, 32m+t+8) are all ones
-#pragma unroll
-        for (int k = 1; k < 8; ++k) y &= __builtin_amdgcn_alignbit(x, nx, 32 - k);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) c8[(8 - r) & 7] += __builtin_popcount(y & (0x80808080u >> r));
-    };
-    uint32_t pend = 0;
-    bool has_pend = false;
-    uint32_t wl = 0;            // workgroup-local bit position of the stage's first word
-    uint32_t lead = 0, pos = 0; // bit position in the stage (lead: the carried partial word's bits)
-    // ---- flush: complete words to R, the partial word carried (as entropy_code_kernel) ----
-    auto flush = [&]() {
-        lds_barrier();  // every string of the stage ORed in
-        const uint32_t ncw = pos >> 5;
-        const uint32_t wbase = wl >> 5;
-        for (uint32_t w = tid; w < ncw; w += kK3Threads) {
-            uint32_t v = L.stage[w];
-            if (w == 0) v |= L.carry;
-            R32[wbase + w] = __builtin_bswap32(v);
-            if (w + 1 < ncw) count_word(v, L.stage[w + 1]);
-        }
-        if (tid == 0) {
-            if (ncw) {
-                const uint32_t w0 = L.stage[0] | L.carry;
-                if (has_pend) count_word(pend, w0);
-                pend = ncw == 1 ? w0 : L.stage[ncw - 1];
-                has_pend = true;
-            }
-            uint32_t v = L.stage[ncw];
-            if (ncw == 0) v |= L.carry;
-            L.carry = v;
-        }
-        lds_barrier();
-        for (uint32_t w = tid; w <= ncw; w += kK3Threads) L.stage[w] = 0;
-        lds_barrier();
-        wl += pos - lead;
-        lead = wl & 31;
-        pos = lead;
-    };
-    auto or_bits = [&](uint32_t off, uint32_t s, uint32_t n) {  // n in [1, 27]: s MSB-first at stage bit off
-        const uint32_t v = s << (32 - n), sh = off & 31, w = off >> 5;
-        atomicOr(&L.stage[w], v >> sh);
-        if (sh + n > 32) atomicOr(&L.stage[w + 1], v << (32 - sh));
-    };
-
-    uint4 cur = load_chunk((uint32_t)wv);
-    int dcs = load_dc((uint32_t)wv);
-    uint32_t par = 0;
-    lds_barrier();  // the tables, the zeroed stage
-    uint64_t tq = JPGE_NOW();
-    for (uint32_t r = 0; r < nrounds; ++r) {
-        const uint32_t ci = r * kCWaves + (uint32_t)wv;            // this wave's chunk
-        const uint32_t c0 = ci * kCChunk;                          // its first block (workgroup-relative)
-        const uint32_t nb = c0 < nblk ? min((uint32_t)kCChunk, nblk - c0) : 0u;
-        // ---- stage the chunk, fetch the next round's ----
-        wave_order();
-        st4[lane] = cur;
-        cur = load_chunk(ci + kCWaves);
-        // ---- per block fields, lane j = block j of the chunk ----
-        const uint32_t g = B0 + c0 + (uint32_t)lane;  // (frame block)
-        const uint32_t m6 = g / bpm, k = g - m6 * bpm;
-        const int comp = block_comp((int)k, bpm);
-        const uint32_t tsel_v = comp != 0 ? 512u : 0u;
-        int dd;
-        {
-            const bool ynext = k >= 1 && k < bpm - 2;
-            const int back = ynext ? 1 : (k == 0 ? 3 : (int)bpm);
-            const bool none = !ynext && g < bpm;
-            bool reset = false;
-            if (a.rst.mcus && (k == 0 || k >= bpm - 2)) reset = (m6 + a.rst.mcu0) % a.rst.mcus == 0;
-            const int dcv = __builtin_amdgcn_ds_bpermute((lane + 6) * 4, dcs);
-            int pd = __builtin_amdgcn_ds_bpermute((lane + 6 - back) * 4, dcs);  // (lane - back >= -6)
-            pd = reset ? 0 : none ? (comp == 0 ? a.seed.v[0] : comp == 1 ? a.seed.v[1] : a.seed.v[2]) : pd;
-            dd = (int)(int16_t)dcv - (int)(int16_t)pd;
-        }
-        dcs = load_dc(ci + kCWaves);
-        // each block's DC difference over its DC coefficient (lanes past the chunk: a slot of their own)
-        st16[(uint32_t)lane < (uint32_t)kCChunk ? (uint32_t)lane * 64u : 512u + (uint32_t)lane] = (int16_t)dd;
-        wave_order();
-        JPGE_ACC(1, tq);
-        // ---- the chunk's strings: in-chunk offsets by wave scans ----
-        uint32_t w1[kCChunk], w2[kCChunk];  // string | length << 27; offset in the chunk | ZRL count << 16
-        uint32_t wpos = 0, zmask = 0;
-#pragma unroll
-        for (int jb = 0; jb < kCChunk; ++jb) {
-            w1[jb] = 0;
-            w2[jb] = 0;
-            if ((uint32_t)jb >= nb) continue;
-            const int c = st16[jb * 64 + natoff];
-            const uint64_t B1 = __ballot(c != 0) | 1ull;  // the AC non-zeros, and bit 0 (lane 0: the DC)
-            const uint64_t M = B1 & ~1ull;
-            const bool inM = __builtin_amdgcn_inverse_ballot_w64(M);
-            // run: exact up to 31 from the 32 mask bits below p (a 1 below them); a run
-            // of 16+ sends the block to the exact form, which also codes its ZRLs
-            uint32_t run = (uint32_t)__builtin_clz((uint32_t)((B1 << shl) >> 32) | 1u);
-            const bool zb = (__ballot(run >= 16u) & M) != 0;
-            const uint32_t tsel = __builtin_amdgcn_readlane(tsel_v, jb);
-            const int cat = __builtin_amdgcn_frexp_expf((float)c);
-            uint32_t nz = 0, zl = 0;
-            if (zb) {
-                run = (uint32_t)__builtin_clzll(B1 << shl);
-                nz = inM ? run >> 4 : 0u;
-                zl = (L.tab[tsel + 256u + 0xF0u] >> 16) & 0xFFu;
-                zmask |= 1u << jb;
-            }
-            const uint32_t rr = inM ? (run & 15u) : 0u;
-            const uint32_t ent = L.tab[tsel + tdc + ((rr << 4) | (uint32_t)cat)];
-            const bool has = inM || lane == 0 || lane == 63;  // DC, non-zeros, EOB
-            const uint32_t len = has ? (ent >> 16) & 0xFFu : 0u;
-            const uint32_t str = ((ent & 0xFFFFu) << (ent >> 24)) | extra_bits(c, cat);
-            const uint32_t tot = len + nz * zl;
-            const uint32_t incl = wave_scan_incl(tot);
-            w1[jb] = str | (len << 27);
-            w2[jb] = (wpos + incl - tot) | (nz << 16);
-            wpos += __builtin_amdgcn_readlane(incl, 63);
-        }
-        JPGE_ACC(3, tq);
-        // ---- place the chunks in the round (one barrier; the totals alternate) ----
-        if (lane == 0) L.wtot[par][wv] = wpos;
-        lds_barrier();
-        uint32_t base = 0, T = 0;
-#pragma unroll
-        for (int w = 0; w < kCWaves; ++w) {
-            const uint32_t s = L.wtot[par][w];
-            if (w < wv) base += s;
-            T += s;
-        }
-        par ^= 1u;
-        if (pos + T > kCStageBits) flush();
-        JPGE_ACC(4, tq);
-        const uint32_t gb = pos + base;
-#pragma unroll
-        for (int jb = 0; jb < kCChunk; ++jb) {
-            if ((uint32_t)jb >= nb) continue;
-            const uint32_t v1 = w1[jb], len = v1 >> 27;
-            uint32_t off = gb + (w2[jb] & 0xFFFFu);
-            if (zmask & (1u << jb)) {  // ZRL codes ahead of the lane's symbol (rare)
-                const uint32_t nz = w2[jb] >> 16;
-                const uint32_t ze = L.tab[__builtin_amdgcn_readlane(tsel_v, jb) + 256u + 0xF0u];
-                const uint32_t zl = (ze >> 16) & 0xFFu;
-                for (uint32_t z = 0; z < nz; ++z, off += zl) or_bits(off, ze & 0xFFFFu, zl);
-            }
-            if (len) or_bits(off, v1 & 0x7FFFFFFu, len);
-        }
-        pos += T;
-        JPGE_ACC(6, tq);
-    }
-    flush();
-    const uint32_t Lb = wl;  // this workgroup's bits (>= 6: every block codes >= 2 bits, >= 3 blocks)
-    if (tid == 0 && (Lb & 31)) R32[Lb >> 5] = __builtin_bswap32(L.carry);
-    vm_drain();
-    __syncthreads();
-    JPGE_STAMP(1);
-    // ---- 0xFF bytes of the stream at each byte alignment b (as entropy_code_kernel) ----
-    if (tid == 0) {
-        const uint32_t tail = (Lb & 31) ? L.carry : 0u;
-        if (has_pend) count_word(pend, tail);
-        if (Lb & 31) count_word(tail, 0u);
-    }
-    {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            uint32_t s = c8[b];
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-            if (lane == 0 && s) atomicAdd(&L.cnt8[b], s);
-        }
-    }
-    __syncthreads();
-    write_wg_record(a, wg, G, R8, Lb, L.cnt8, &L.carry, L.wtot[0], tid);
-    JPGE_STAMP(2);
-}
-
 // ---- record scan: bit offsets, byte splits and 0xFF prefixes ----
 // A byte belongs to the workgroup holding its last bit.  The byte split between
 // records k-1 and k (alignment b_k = P_k & 7 != 0) is rebuilt from k-1's last b_k
@@ -1185,8 +932,6 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* tco
 
 hipError_t launch_entropy_code(const EntropyArgs& a, hipStream_t s, const KTimer* tcode) {
     const uint32_t G = a.seg.grid();
-    if (!a.recs)
-        return launch_timed(tcode, entropy_coef_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&a, 1, G));
     return launch_timed(tcode, entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), s, frame_set<1>(&a, 1, G));
 }
 
@@ -1214,8 +959,7 @@ hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s, const 
         const EntropyArgs& m = a[f];
         if (m.seg.grid() != G || !m.done || !m.place || m.rst.mcus || G > kPlaceInCodeMaxWgs) return hipErrorInvalidValue;
     }
-    hipError_t e = a[0].recs ? launch_timed(tcode, entropy_code_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), s, fs)
-                             : launch_timed(tcode, entropy_coef_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), s, fs);
+    hipError_t e = launch_timed(tcode, entropy_code_kernel<kMaxSet>, dim3(G * n), dim3(kK3Threads), s, fs);
     if (e != hipSuccess) return e;
     for (int f = 0; f < n; ++f) {
         fs.a[f].flags |= kExtPlace;
@@ -1227,8 +971,7 @@ hipError_t launch_entropy_set(const EntropyArgs* a, int n, hipStream_t s, const 
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s) {
     const uint32_t G = a.seg.grid();
     if (!a.summary) return hipErrorInvalidValue;
-    if (a.recs) hipLaunchKernelGGL(entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), 0, s, frame_set<1>(&a, 1, G));
-    else hipLaunchKernelGGL(entropy_coef_kernel<1>, dim3(G), dim3(kK3Threads), 0, s, frame_set<1>(&a, 1, G));
+    hipLaunchKernelGGL(entropy_code_kernel<1>, dim3(G), dim3(kK3Threads), 0, s, frame_set<1>(&a, 1, G));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // (restart intervals: the stripe's placement is its own, computed now; its summary

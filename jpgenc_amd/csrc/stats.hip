@@ -80,9 +80,7 @@ struct K2WLds {
     uint32_t next;                                       // the next sub-stream to take
 };
 
-// kRecs: also write the symbol records (the record-reading code kernel); without them
-// (a.recs == nullptr) the code kernel re-derives the symbols from the coefficients.
-template <int kN, bool kRecs>
+template <int kN>
 __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe))) void stats_wave_kernel(FrameSet<StatsArgs, kN> fs) {
     const uint32_t set_f = (kN == 1 ? 0u : set_member_rolled(fs.wg0, fs.n, blockIdx.x));  // (frame sets: kernels.hpp)
     const StatsArgs& a = fs.a[set_f];
@@ -273,8 +271,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 b.rk += zi;
                 if (nzr) {
                     const uint32_t zrec = b.Tj | (0xF0u << 16);
-                    if constexpr (kRecs)
-                        for (uint32_t z = 1; z <= nzr; ++z) srec[base + b.rk - z] = zrec;
+                    for (uint32_t z = 1; z <= nzr; ++z) srec[base + b.rk - z] = zrec;
                     const uint32_t wz = b.acw + kRunStride * 15u;  // (symbol 0xF0)
                     atomicAdd(&cnt[wz], nzr);
                     const uint32_t kz = b.acbj + k2p - 1u;
@@ -282,7 +279,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 }
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b.em)) {
-                if constexpr (kRecs) srec[base + b.rk] = b.rec;
+                srec[base + b.rk] = b.rec;
                 atomicAdd(&cnt[b.w], 1u);
                 const uint32_t kk = b.acbj + k2p;
                 if (kk < L.key[b.w]) atomicMin(&L.key[b.w], kk);
@@ -314,10 +311,8 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                     // are masked off
                     baseB = base + (uint32_t)__builtin_popcountll(A.em);
                     const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
-                    if constexpr (kRecs) {
-                        __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
-                    }
+                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
                     if (ia) atomicAdd(&cnt[A.w], 1u);
                     if (ib) atomicAdd(&cnt[B.w], 1u);
                     // (every lane reads its word: a lane without a record has c = 0, so its
@@ -341,7 +336,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             if (jb < j1) base += emit(cp[0], jb, base);  // an odd last block
         }
         JPGE_ACC(2, tq);
-        if (kRecs && lane == 0) a.tcount[s] = base;
+        if (lane == 0) a.tcount[s] = base;
         si = sn;
         JPGE_ACC(3, tq);
     }
@@ -410,8 +405,7 @@ static hipError_t launch_stats_fs(const FrameSet<StatsArgs, kN>& fs, hipStream_t
         if ((uint64_t)fs.a[f].g.nblocks() * 128 >= (1ull << 32)) return hipErrorInvalidValue;
         if (fs.wg0[f + 1] - fs.wg0[f] != stats_grid(fs.a[f].seg, fs.a[f].wgs)) return hipErrorInvalidValue;
     }
-    if (fs.a[0].recs) return launch_timed(t, stats_wave_kernel<kN, true>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
-    return launch_timed(t, stats_wave_kernel<kN, false>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
+    return launch_timed(t, stats_wave_kernel<kN>, dim3(fs.wg0[fs.n]), dim3(kWThreads), s, fs);
 }
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s, const KTimer* t) {
