@@ -59,6 +59,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Boost, absent here and on the GPU box, so it cannot be rebuilt beside the GPU.
 REF_CPU_4K_Q90 = {"value": 4.4, "unit": "MPix/s", "cores": 8, "kind": "reference",
                   "source": "BASELINE.md §2 (reference writeJPEG, 3840x2160 Q90, 8 vCPU Xeon, survey container)"}
+REF_CPU_1080_Q90 = {"value": 3.8, "unit": "MPix/s", "cores": 8, "kind": "reference",
+                    "source": "BASELINE.md §2 (reference writeJPEG, 1920x1080 Q90: 550 ms, 8 vCPU Xeon, survey container)"}
+REF_CPU_16K_Q90 = {"value": 3.6, "unit": "MPix/s", "cores": 8, "kind": "reference",
+                   "source": "BASELINE.md §2 (reference writeJPEG, 16384x16384 Q90, single interval: 74.5 s, 8 vCPU "
+                             "Xeon, survey container)"}
 
 
 # subsampling modes (jpge.h JPGE_S*) -> the name in the metric / workload
@@ -104,6 +109,11 @@ def parse(argv=None):
                     help="rehearse N ranks on fewer than N GPUs (ranks share devices; the line says so). "
                          "Without it, --gpus N refuses to run on a node with fewer than N GPUs")
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: time without per-kernel events")
+    ap.add_argument("--pg-timeout", type=float, default=120.0,
+                    help="seconds a gloo / RCCL collective may wait before it fails (process groups' timeout)")
+    ap.add_argument("--phase-timeout", type=float, default=420.0,
+                    help="seconds a rank may spend in one phase (setup, warm-up, timed steps, ...) before it "
+                         "exits with status 124, naming the phase (0 = no watchdog)")
     ap.add_argument("--event-every", type=int, default=1024,
                     help="in the timed region, launch the kernels of the frame set holding every N-th frame with "
                          "timing events (the in-situ diagnostic; events cost throughput and host CPU: a HIP "
@@ -150,7 +160,52 @@ def spawn(n: int, argv: list[str]) -> int:
     return rc
 
 
-def dist_setup(n_gpus: int):
+class PhaseWatch:
+    """Names the phase each rank is in and ends a rank stuck in one: a
+    daemon thread checks once a second; a phase older than its limit prints the rank, the
+    phase and the time to stderr and exits the process with status 124, so a first
+    multi-GPU run that stalls (RCCL setup, a p2p transfer, a barrier) ends well inside the
+    driver's own limit and says where.  (os._exit: no GPU teardown, no exec.)"""
+
+    def __init__(self, limit_s: float):
+        import threading
+
+        self.limit = limit_s
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.name, self.t0 = "start", time.monotonic()
+        self.extra = {}
+        self.lock = threading.Lock()
+        if limit_s > 0:
+            threading.Thread(target=self._run, daemon=True).start()
+
+    def __call__(self, name: str, limit_s: float | None = None) -> None:
+        with self.lock:
+            self.name, self.t0 = name, time.monotonic()
+            self.extra[name] = limit_s
+
+    def _run(self):
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                name, t0 = self.name, self.t0
+                lim = self.extra.get(name) or self.limit
+            dt = time.monotonic() - t0
+            if dt > lim:
+                print(f"bench: rank {self.rank}: phase '{name}' exceeded its {lim:.0f} s limit ({dt:.0f} s); "
+                      f"exiting with status 124", file=sys.stderr, flush=True)
+                os._exit(124)
+
+
+PHASE = PhaseWatch(0)  # (main() replaces it with the --phase-timeout watch)
+
+
+def pg_timeout(args):
+    import datetime
+
+    return datetime.timedelta(seconds=max(10, int(args.pg_timeout)))
+
+
+def dist_setup(n_gpus: int, args=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -161,14 +216,19 @@ def dist_setup(n_gpus: int):
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        PHASE("init_process_group (gloo rendezvous)")
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=pg_timeout(args) if args is not None else None)
         pg = dist
     return rank, local, world, pg
 
 
 def barrier(pg):
     if pg is not None:
+        name = PHASE.name
+        PHASE(f"barrier after '{name}'")
         pg.barrier()
+        PHASE(name)
 
 
 def max_over_ranks(pg, v: float) -> float:
@@ -253,13 +313,15 @@ def rank_lanes(args, world: int) -> int:
     return max(1, 6 // per_device) if per_device > 1 else 0
 
 
-def gather_group(world: int):
+def gather_group(world: int, args=None):
     """Process group for the data-path collectives: RCCL ("nccl") when every rank
     has its own GPU, else gloo (ranks sharing a GPU; tensors staged through the host)."""
     import torch
     import torch.distributed as dist
 
-    return dist.new_group(backend="nccl" if visible_devices() >= world else "gloo")
+    backend = "nccl" if visible_devices() >= world else "gloo"
+    PHASE(f"new_group ({backend})")
+    return dist.new_group(backend=backend, timeout=pg_timeout(args) if args is not None else None)
 
 
 def frame_seed(rank: int, i: int) -> int:
@@ -278,37 +340,13 @@ def batch_share(total: int, rank: int, world: int) -> list[int]:
 # ---------------------------------------------------------------- CPU baseline
 
 def cpu_baseline(args) -> tuple[dict, dict]:
-    """The test-only oracle (CPU restatement of the reference path) on a bounded
-    sample of the same workload: whole 4K Q90 frames until ~cpu_seconds.  Also
-    returns {frame index: sha256 of the oracle's bytes} for the output check."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import _oracle  # noqa: E402
+    """The 4k-frames workload's baseline: whole frames of the step's inputs (seeds 3..)."""
     import jpgenc_amd as J
 
-    threads = min(16, os.cpu_count() or 1)
-    _oracle.orc().orc_set_threads(threads)
-    enc_times = []  # encode-only time per frame (synthesis excluded)
-    hashes = {}
-    for i in range(16):
-        rgb = J.synth_rgb8(frame_seed(0, i), args.width, args.height)
-        s = time.perf_counter()
-        out = _oracle.encode(rgb, args.quality, subsampling=args.subsampling)
-        enc_times.append(time.perf_counter() - s)
-        hashes[i] = hashlib.sha256(out).hexdigest()
-        if sum(enc_times) >= args.cpu_seconds:
-            break
-    px = args.width * args.height * len(enc_times)
-    return {
-        "value": round(px / sum(enc_times) / 1e6, 3),
-        "unit": "MPix/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{len(enc_times)} x {args.width}x{args.height} {sub_name(args)} Q{args.quality} frames (seeds 3..), "
-                  f"oracle/jpge_oracle.cpp restatement, OpenMP {threads} threads (DCT/quant parallel, "
-                  f"like the reference)",
-        "reference": REF_CPU_4K_Q90 if (args.width, args.height, args.quality, args.subsampling) ==
-        (W4K, H4K, 90, 420) else None,
-    }, hashes
+    ref = REF_CPU_4K_Q90 if (args.width, args.height, args.quality, args.subsampling) == (W4K, H4K, 90, 420) else None
+    return oracle_cpu_baseline(args, lambda i: J.synth_rgb8(frame_seed(0, i), args.width, args.height),
+                               f"{args.width}x{args.height} {sub_name(args)} Q{args.quality} frames (seeds 3..)", ref,
+                               subsampling=args.subsampling, want_hashes=True)
 
 
 def sub_name(args) -> str:
@@ -419,12 +457,169 @@ def load_pmc_traffic(profile_dir: str, width: int, height: int) -> dict:
     return out
 
 
-def host_cpu_use(cg0: dict, cg1: dict, dt: float):
-    if not cg0:
+def cgroup_quota_cpus():
+    """The cgroup's CPU quota in CPUs (cpu.max: quota / period), None when unlimited or
+    not visible."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
         return None
-    return {"cpus_used": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e6 / dt, 2),
+
+
+def host_cpu_use(cg0: dict, cg1: dict, dt: float, world: int = 1):
+    """The cgroup's CPU use over the timed region (every rank of this box shares it), its
+    quota and throttling, and CPUs per rank."""
+    if not cg0:
+        return {"cpus_used": None, "quota_cpus": cgroup_quota_cpus(), "reason": "cgroup cpu.stat not visible"}
+    used = (cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e6 / dt
+    return {"cpus_used": round(used, 2), "quota_cpus": cgroup_quota_cpus(),
+            "cpus_per_rank": round(used / max(1, world), 2), "ranks_in_cgroup": world,
             "throttled_periods": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
             "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3, 1)}
+
+
+
+# ---------------------------------------------------------------- kernel rooflines
+
+def solo_timing(J, local, frames, outd, args, fset: int, restart: int = 0):
+    """After the timed region: the given frames through a 1-lane encoder (nothing else on
+    the GPU), every launch with its own HIP events bound to its dispatch, in frame sets of
+    `fset` (the pipeline's launch shape; 1 = one frame per launch).  Returns the encoder's
+    timing and the CLOCK_MONOTONIC window (rocprofv3 timestamps use the same clock)."""
+    env = {"JPGE_SET": str(fset)}
+    if fset > 1:  # (a 1-lane encoder places by the pack kernels unless told otherwise; sets place in the code kernel)
+        env["JPGE_EXT_PLACE"] = "1"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        solo = J.Encoder(local, lanes=1)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    solo.set_subsampling(getattr(args, "subsampling", 420))
+    if restart:
+        solo.set_restart(restart)
+    # warm-up batches first: right after a multi-lane region the chip's clock is still
+    # settling (K1, fp64 VALU, ran its first solo batch ~1-2 us slower)
+    for _ in range(max(1, args.solo_warmup)):
+        solo.encode_batch_dev(frames, outd, quality=args.quality)
+    solo.set_timing(1)
+    solo.reset_timing()
+    s0 = time.monotonic_ns()
+    for _ in range(args.solo_batches):
+        solo.encode_batch_dev(frames, outd, quality=args.quality)
+    win = [s0, time.monotonic_ns()]
+    tm = solo.timing()
+    solo.close()
+    return tm, win
+
+
+def alg_bytes(npx: float, cb: float, rec_bytes: float, avg_jpeg: float):
+    """Per-kernel and entropy-stage algorithmic bytes per frame: K1 reads
+    RGB8 and writes int16 coefficients; K2 reads the coefficients and writes one 4-byte
+    record per Huffman-coded symbol; the code kernel reads the records and writes the bit
+    stream (~ the .jpg size); the pack kernel reads it and writes the stuffed bytes."""
+    alg = {
+        "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
+        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 4 B each"),
+        "entropy_code_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + bit stream written (~.jpg size)"),
+        "entropy_pack_kernel": (2.0 * avg_jpeg, "bit stream read + stuffed .jpg bytes written"),
+    }
+    stage = {"entropy_stage": (rec_bytes + avg_jpeg, "symbol records read 4 B each + .jpg bytes written")}
+    return alg, stage
+
+
+TM_KEY = {"fdct_kernel": "fdct_sum", "stats_kernel": "dc_stats_sum", "entropy_code_kernel": "code_sum",
+          "entropy_pack_kernel": "pack_sum", "entropy_stage": "entropy_sum"}
+PMC_KEY = {"entropy_stage": "entropy_kernel"}
+
+
+def kernel_rooflines(tm, alg, stage_alg, traffic, npx):
+    """Per launch (a frame set's launch covers frames_per_launch frames: its bytes and its
+    duration both); traffic (PMC, profiles/) is per frame."""
+    nl = max(1, tm.get("launches") or tm["frames"])
+    fpl = tm["frames"] / nl if tm["frames"] else 1.0
+    out = {}
+    timed = bool(tm.get("launches") or tm["frames"])
+    for name, (b, what) in list(alg.items()) + list(stage_alg.items()):
+        ms = tm[TM_KEY[name]] / nl
+        bl = b * fpl
+        tr = traffic.get(PMC_KEY.get(name, name))
+        if not timed or ms <= 0:  # (no launch of this pass was timed: no figure, not a zero)
+            out[name] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                         "traffic": int(tr * fpl) if tr else tr, "alg_bytes_per_launch": int(bl),
+                         "alg_bytes": what, "avg_kernel_ms": None, "timed_launches": 0,
+                         "reason": "no launch of this kernel was timed in this pass (kernel events off or "
+                                   "no sampled frame)"}
+            continue
+        ach = bl / (ms * 1e-3) / 1e9
+        out[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(tr * fpl) if tr else tr,
+                     "alg_bytes_per_launch": int(bl), "alg_bytes": what, "avg_kernel_ms": round(ms, 5),
+                     "timed_launches": nl, "frames_per_launch": round(fpl, 3)}
+    # the north star's "HBM-read roofline": K1's RGB8 read alone (3 B/px)
+    k1 = out["fdct_kernel"]
+    ms1 = tm["fdct_sum"] / nl
+    if ms1 > 0:
+        rd = 3.0 * npx * fpl / (ms1 * 1e-3) / 1e9
+        k1["read_achieved"] = round(rd, 1)
+        k1["read_frac"] = round(rd / HBM_PEAK_GBS, 4)
+    return out
+
+
+def solo_headline(stages_solo, alg, frames_per_step: float, ms_step: float):
+    """The headline roofline: the dominant kernel (longest exclusive time) ALONE on the GPU
+    (the solo pass), checked against the step: its launches per step x its duration cannot
+    exceed the step, or the run fails."""
+    dominant = max(alg, key=lambda k: stages_solo[k]["avg_kernel_ms"] or 0.0)
+    roofline = dict(kernel=dominant, timing="solo (1-lane encoder after the timed region; HIP events bound "
+                                            "to the kernel's dispatch, hipExtLaunchKernel)", **stages_solo[dominant])
+    lps = frames_per_step / roofline["frames_per_launch"]
+    spent = lps * roofline["avg_kernel_ms"]
+    roofline["check"] = {"launches_per_step": round(lps, 1), "launches_x_avg_ms": round(spent, 3),
+                         "ms_per_step": round(ms_step, 3), "ok": spent <= ms_step}
+    if spent > ms_step:
+        raise SystemExit(f"bench: roofline check failed: {lps:.1f} launches x {roofline['avg_kernel_ms']} ms "
+                         f"= {spent:.3f} ms > {ms_step:.3f} ms per step")
+    return roofline
+
+
+def oracle_cpu_baseline(args, make_frame, label: str, reference: dict | None, restart: int = 0,
+                        subsampling: int = 420, want_hashes: bool = False):
+    """The test-only oracle (CPU restatement of the reference path) on a bounded sample of
+    the workload: frames from make_frame(i) until ~cpu_seconds of encode time (synthesis
+    excluded).  Returns the cpu_baseline object and {i: sha256 of the oracle's bytes}."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle  # noqa: E402
+
+    PHASE("cpu baseline (oracle)")
+    threads = min(16, os.cpu_count() or 1)
+    _oracle.orc().orc_set_threads(threads)
+    enc_times, hashes, px = [], {}, 0
+    for i in range(64):
+        rgb = make_frame(i)
+        t = time.perf_counter()
+        out = _oracle.encode(rgb, args.quality, restart=restart, subsampling=subsampling)
+        enc_times.append(time.perf_counter() - t)
+        px += rgb.shape[0] * rgb.shape[1]
+        if want_hashes:
+            hashes[i] = hashlib.sha256(out).hexdigest()
+        if sum(enc_times) >= args.cpu_seconds:
+            break
+    return {
+        "value": round(px / sum(enc_times) / 1e6, 3),
+        "unit": "MPix/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{len(enc_times)} x {label}, oracle/jpge_oracle.cpp restatement, OpenMP {threads} threads "
+                  f"(DCT/quant parallel, like the reference)",
+        "reference": reference,
+    }, hashes
 
 
 # ---------------------------------------------------------------- workloads
@@ -434,6 +629,9 @@ def run_dist_check(args, rank, local, world, pg):
     JPGE_BENCH_FAIL_RANK=r makes rank r fail before the first barrier)."""
     if os.environ.get("JPGE_BENCH_FAIL_RANK") == str(rank):
         raise SystemExit(3)
+    if os.environ.get("JPGE_BENCH_HANG_RANK") == str(rank):  # (the phase watchdog's test)
+        PHASE("dist-check: stuck (test hook)")
+        time.sleep(3600)
     barrier(pg)
     dt = max_over_ranks(pg, 0.001 * (rank + 1))
     n = sum_over_ranks(pg, 1.0)
@@ -447,7 +645,10 @@ def run_dist_check(args, rank, local, world, pg):
 def run_striped16k(args, rank, local, world, pg):
     """One 16384^2 frame per step: whole-frame encode on one GPU; on N GPUs each
     rank holds and encodes its row stripe, with the three RCCL exchanges and the
-    segment gather of SURVEY 8(e) inside the timed step (output identical to 1 GPU)."""
+    segment gather of SURVEY 8(e) inside the timed step (output identical to 1 GPU).
+    After the timed region each rank's frame (or stripe) runs through a 1-lane encoder
+    with kernel events (the roofline), and at N = 1 the CPU oracle encodes row stripes
+    of the same frame (the CPU baseline)."""
     import torch
 
     import jpgenc_amd as J
@@ -457,14 +658,15 @@ def run_striped16k(args, rank, local, world, pg):
     torch.cuda.set_device(local)
     W = H = 16384
     restart = 1024 if args.restart is None else args.restart
+    PHASE("setup (16K frame, encoder)")
     rgb = J.synth_rgb8(5, W, H)  # SURVEY 8(d) config 5 seed
     cap = J.max_jpeg_bytes(W, H)
     out = torch.empty(cap, dtype=torch.uint8, device=f"cuda:{local}")
     if world == 1:
+        r0, nr = 0, H // 16
         enc = J.Encoder(local)
         enc.set_restart(restart)
         src = torch.from_numpy(rgb.reshape(-1)).to(f"cuda:{local}")
-        del rgb
 
         def step():
             return enc.encode_batch_dev([(src.data_ptr(), W, H, W * 3)], [(out.data_ptr(), cap)],
@@ -472,7 +674,7 @@ def run_striped16k(args, rank, local, world, pg):
     else:
         import torch.distributed as dist
 
-        rccl = gather_group(world)  # the exchanges and the gather ride RCCL over xGMI
+        rccl = gather_group(world, args)  # the exchanges and the gather ride RCCL over xGMI
         r0, nr = stripes.stripe_rows(H // 16, world, stripes.restart_align(W, restart))[rank]
         src = torch.from_numpy(np.ascontiguousarray(rgb[16 * r0:16 * (r0 + nr)]).reshape(-1)).to(f"cuda:{local}")
         del rgb
@@ -482,21 +684,62 @@ def run_striped16k(args, rank, local, world, pg):
         def step():
             return stripes.encode_stripe_dist(enc, src.data_ptr(), W * 3, W, H, args.quality, out, group=rccl,
                                               restart=restart)
+    PHASE("warm-up steps (first RCCL exchanges)" if world > 1 else "warm-up steps")
     for _ in range(args.warmup):
         n = step()
     torch.cuda.synchronize()
     barrier(pg)
+    PHASE("timed steps")
+    cg0 = cgroup_cpu_stat()
+    pc0 = process_cpu_s()
+    win0 = time.monotonic_ns()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         n = step()
     torch.cuda.synchronize()
     barrier(pg)
-    dt = max_over_ranks(pg, time.perf_counter() - t0)
+    dt = time.perf_counter() - t0
+    win1 = time.monotonic_ns()
+    cg1 = cgroup_cpu_stat()
+    rank_cpus = all_gather_floats(pg, (process_cpu_s() - pc0) / dt, world)
+    dt = max_over_ranks(pg, dt)
+    ms_step = dt / args.steps * 1e3
+    # per-kernel rooflines: this rank's rows (the whole frame at N = 1) as one frame through
+    # a 1-lane encoder with kernel events (the same kernels over the same pixels; a stripe's
+    # own phases run them with the exchanges between)
+    roofline = stages_solo = None
+    solo_win = None
+    hs = 16 * nr if world > 1 else H
+    if args.solo_batches > 0 and not args.no_kernel_events:
+        PHASE("solo kernel timing")
+        enc.close()
+        tm_solo, solo_win = solo_timing(J, local, [(src.data_ptr(), W, hs, W * 3)], [(out.data_ptr(), cap)], args, 1,
+                                        restart=restart)
+        sym_enc = J.Encoder(local, lanes=1)
+        hrows = rgb if world == 1 else src.view(hs, W, 3).cpu().numpy()
+        syms = int(sym_enc.symbol_stats(hrows, quality=args.quality)[0].sum())
+        sym_enc.close()
+        del hrows
+        alg, stage_alg = alg_bytes(W * hs, 3.0, 4.0 * syms, float(n) * hs / H)
+        stages_solo = kernel_rooflines(tm_solo, alg, stage_alg, {}, W * hs)
+        roofline = solo_headline(stages_solo, alg, 1, ms_step)
+    else:
+        enc.close()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rows = 1024  # a bounded sample: 16384 x 1024 row stripes of the same frame, the same restart interval
+        cpu, _ = oracle_cpu_baseline(args, lambda i: np.ascontiguousarray(rgb[rows * (i % (H // rows)):
+                                                                              rows * (i % (H // rows) + 1)]),
+                                     f"{W}x{rows} row stripes of the 16384^2 frame (seed 5), "
+                                     + (f"restart interval {restart} MCUs" if restart else "single interval"),
+                                     REF_CPU_16K_Q90 if args.quality == 90 and not restart else None, restart=restart)
+        if cpu["reference"] is None and args.quality == 90:
+            cpu["reference_single_interval"] = REF_CPU_16K_Q90
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": f"MPixels/s encode (16K 4:2:0 Q={args.quality})",
             "value": round(W * H * args.steps / dt / 1e6, 1), "unit": "MPix/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 photo-like frame, seed 5, HBM-resident)",
             "config": {"workload": f"16384x16384 4:2:0 Q{args.quality}, one frame per step, "
@@ -507,9 +750,19 @@ def run_striped16k(args, rank, local, world, pg):
                                          if restart else
                                          "DC seeds, histogram sum/min, summaries; segments gathered to rank 0)")),
                        "restart_mcus": restart, "jpeg_bytes": int(n)},
+            "roofline": roofline,
+            "roofline_dct_stage": dict(kernel="fdct_kernel", timing="solo", **stages_solo["fdct_kernel"])
+            if stages_solo else None,
+            "stages_solo": stages_solo,
+            "solo_rows": hs,
+            "host_cpu": host_cpu_use(cg0, cg1, dt, world),
+            "rank_cpus": [round(c, 2) for c in rank_cpus],
+            "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win},
             "devices": args.devices,
-        }), flush=True)
-    enc.close()
+        }
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
+        print(json.dumps(line), flush=True)
 
 
 def run_ppm_files(args, rank, local, world, pg):
@@ -589,6 +842,7 @@ def run_batch1080(args, rank, local, world, pg):
     W, H, B = 1920, 1080, args.frames or 256
     share = batch_share(B, rank, world)
     cap = out_capacity(J, W, H)
+    PHASE("setup (frames, encoder, gather)")
     host = {i: J.synth_rgb8(batch_seed(i), W, H) for i in share}
     ins = {i: torch.from_numpy(host[i].reshape(-1)).to(dev) for i in share}
     frames = [(ins[i].data_ptr(), W, H, W * 3) for i in share]
@@ -600,13 +854,16 @@ def run_batch1080(args, rank, local, world, pg):
 
         from jpgenc_amd.gather import BatchGather
 
-        meta = dist.new_group(backend="gloo")
+        PHASE("new_group (gloo, lengths)")
+        meta = dist.new_group(backend="gloo", timeout=pg_timeout(args))
         if args.devices["shared"]:  # ranks on one GPU: RCCL refuses them; rank 0's buffers over HIP IPC
+            PHASE("gather setup (HIP IPC handles)")
             gather = BatchGather(None, meta, rank, world, B, len(share) * cap, dev, transport="ipc")
             if gather.transport != "ipc":  # (no IPC: stage through the host over gloo)
-                gather = BatchGather(dist.new_group(backend="gloo"), meta, rank, world, B, len(share) * cap, "cpu")
+                gather = BatchGather(dist.new_group(backend="gloo", timeout=pg_timeout(args)), meta, rank, world, B,
+                                     len(share) * cap, "cpu")
         else:
-            gather = BatchGather(gather_group(world), meta, rank, world, B, len(share) * cap, dev)
+            gather = BatchGather(gather_group(world, args), meta, rank, world, B, len(share) * cap, dev)
         transport = gather.transport if gather.cuda else "gloo (host-staged)"
         nsets = 2  # output slots alternate, so the next encode never waits for this step's pack
     outbuf = torch.empty(nsets * len(share) * cap, dtype=torch.uint8, device=dev)
@@ -634,18 +891,21 @@ def run_batch1080(args, rank, local, world, pg):
         phase["gather_post"] += t3 - t2
         return lens, s
 
+    PHASE("warm-up steps (first RCCL transfers)" if gather is not None else "warm-up steps")
     for _ in range(args.warmup):
         step()
     if gather is not None:
         gather.wait()
     torch.cuda.synchronize()
     barrier(pg)
+    PHASE("timed steps")
     phase.clear()
     if gather is not None:
         gather.lens_wait_s = 0.0
     cg0 = cgroup_cpu_stat()
     pc0 = process_cpu_s()
     th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
+    win0 = time.monotonic_ns()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         lens, s_last = step()
@@ -655,6 +915,7 @@ def run_batch1080(args, rank, local, world, pg):
     torch.cuda.synchronize()
     barrier(pg)
     dt = time.perf_counter() - t0
+    win1 = time.monotonic_ns()
     phase["final_wait"] = dt - (t1 - t0)
     cg1 = cgroup_cpu_stat()
     pcpu = (process_cpu_s() - pc0) / dt
@@ -668,6 +929,7 @@ def run_batch1080(args, rank, local, world, pg):
     # host-path encode of that frame (rank 0's own frames are in its output slots)
     bad = 0
     if not args.no_verify and (world == 1 or gather is not None):
+        PHASE("verification")
         if rank == 0:
             for i in range(B):
                 ref = enc.encode(host[i] if i in host else J.synth_rgb8(batch_seed(i), W, H), quality=args.quality)
@@ -679,6 +941,30 @@ def run_batch1080(args, rank, local, world, pg):
                 if not torch.equal(got, torch.frombuffer(bytearray(ref), dtype=torch.uint8).to(dev)):
                     bad += 1
         bad = int(sum_over_ranks(pg, float(bad)))
+    # per-kernel rooflines: this rank's frames through a 1-lane encoder after the timed
+    # region, in the pipeline's launch shape (sets of 4 1080p frames) and one per launch
+    ms_step = dt_max / args.steps * 1e3
+    stages_solo = stages_solo1 = roofline = None
+    solo_win = solo1_win = None
+    if args.solo_batches > 0 and not args.no_kernel_events and share:
+        PHASE("solo kernel timing")
+        sfr = frames[:min(len(frames), 32)]
+        sout = outd[0][:len(sfr)]
+        fset = max(1, min(4, (4 * 3840 * 2160) // (W * H)))
+        tm_solo, solo_win = solo_timing(J, local, sfr, sout, args, fset)
+        tm_solo1, solo1_win = solo_timing(J, local, sfr, sout, args, 1)
+        syms = [int(enc.symbol_stats(host[i], quality=args.quality)[0].sum()) for i in share[:len(sfr)]]
+        avg_jpeg_rank = sum(lens) / max(1, len(lens))
+        alg, stage_alg = alg_bytes(W * H, 3.0, 4.0 * sum(syms) / len(syms), avg_jpeg_rank)
+        traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H)
+        stages_solo = kernel_rooflines(tm_solo, alg, stage_alg, traffic, W * H)
+        stages_solo1 = kernel_rooflines(tm_solo1, alg, stage_alg, traffic, W * H)
+        roofline = solo_headline(stages_solo, alg, len(share), ms_step)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, _ = oracle_cpu_baseline(args, lambda i: host[i] if i in host else J.synth_rgb8(batch_seed(i), W, H),
+                                     f"{W}x{H} 4:2:0 Q{args.quality} frames of the batch (seeds 1000..)",
+                                     REF_CPU_1080_Q90 if args.quality == 90 else None)
     if rank == 0:
         line = {
             "metric": f"MPixels/s encode (batch of {B} x 1920x1080 4:2:0 Q={args.quality})",
@@ -696,12 +982,21 @@ def run_batch1080(args, rank, local, world, pg):
                 "frames": B, "mismatches": bad,
                 "method": "every frame of the last step, as gathered on rank 0, byte-compared with the host-path "
                           "encode of the same frame"},
-            "host_cpu": host_cpu_use(cg0, cg1, dt),
+            "host_cpu": host_cpu_use(cg0, cg1, dt, world),
             "rank_cpus": [round(c, 2) for c in rank_cpus],
             "rank0_phases_ms_per_step": {k: round(v / args.steps * 1e3, 3) for k, v in phase.items()},
             "lanes_per_rank": enc.lanes(),
             "devices": args.devices,
+            # the dominant kernel alone (rank 0's frames; exclusive time, checked against the step)
+            "roofline": roofline,
+            "roofline_dct_stage": dict(kernel="fdct_kernel", timing="solo", **stages_solo["fdct_kernel"])
+            if stages_solo else None,
+            "stages_solo": stages_solo,
+            "stages_solo_single_frame": stages_solo1,
+            "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win, "solo_single": solo1_win},
         }
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     enc.close()
     if bad:
@@ -725,6 +1020,7 @@ def run_frames(args, rank, local, world, pg):
     pitch = W * 3
     cap = out_capacity(J, W, H)
     # HBM-resident input ring and output slots (torch = device-memory plumbing)
+    PHASE("setup (frames, encoder)")
     host = [J.synth_rgb8(frame_seed(rank, i), W, H) for i in range(D)]
     ins = [torch.from_numpy(h.reshape(-1)).to(dev) for h in host]
     outbuf = torch.empty(F * cap, dtype=torch.uint8, device=dev)
@@ -732,10 +1028,12 @@ def run_frames(args, rank, local, world, pg):
     frames = [(ins[i % D].data_ptr(), W, H, pitch) for i in range(F)]
     outd = [(outbuf.data_ptr() + i * cap, cap) for i in range(F)]
 
+    PHASE("warm-up steps")
     for _ in range(args.warmup):
         enc.encode_batch_dev(frames, outd, quality=args.quality)
     torch.cuda.synchronize()
 
+    PHASE("timed steps")
     enc.set_timing(0 if args.no_kernel_events else args.event_every)
     enc.reset_timing()
     barrier(pg)
@@ -745,6 +1043,7 @@ def run_frames(args, rank, local, world, pg):
     total_bytes = 0
     step_t = []
     cg0 = cgroup_cpu_stat()
+    pc0 = process_cpu_s()
     th0 = thread_cpu() if os.environ.get("JPGE_BENCH_THREADS") else {}
     sampler = ThreadSampler() if os.environ.get("JPGE_BENCH_THREADS") == "2" else None
     for _ in range(args.steps):
@@ -757,6 +1056,7 @@ def run_frames(args, rank, local, world, pg):
     dt = time.perf_counter() - t0
     win1 = time.monotonic_ns()
     cg1 = cgroup_cpu_stat()
+    rank_cpus = all_gather_floats(pg, (process_cpu_s() - pc0) / dt, world)
     if sampler:
         sampler.stop()
     thread_report(th0, dt)
@@ -772,6 +1072,7 @@ def run_frames(args, rank, local, world, pg):
     verified = None
     refs = {}
     if not args.no_verify:
+        PHASE("verification")
         for d in range(D):
             refs[d] = enc.encode(host[d], quality=args.quality)
         bad = 0
@@ -791,6 +1092,7 @@ def run_frames(args, rank, local, world, pg):
     # D distinct frames per step, outputs copied into pinned host buffers.
     d2h = None
     if args.d2h_steps > 0:
+        PHASE("d2h pass")
         hostout = torch.empty(D * cap, dtype=torch.uint8, pin_memory=True)
         hfr = frames[:D]
         hout = [(hostout.data_ptr() + i * cap, cap) for i in range(D)]
@@ -814,46 +1116,17 @@ def run_frames(args, rank, local, world, pg):
     tm_solo = tm_solo1 = None
     solo_win = solo1_win = None
     set_size = max(1, min(4, (4 * 3840 * 2160) // (W * H))) if D >= 2 else 1
-
-    def solo_pass(fset):
-        env = {"JPGE_SET": str(fset)}
-        if fset > 1:  # (a 1-lane encoder places by the pack kernels unless told otherwise; sets place in the code kernel)
-            env["JPGE_EXT_PLACE"] = "1"
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
-        try:
-            solo = J.Encoder(local, lanes=1)
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-        solo.set_subsampling(args.subsampling)
-        sfr, sout = frames[:D], outd[:D]
-        # warm-up batches first (~20 ms at 4K): right after the 4-lane region the chip's
-        # clock is still settling, and K1 (fp64 VALU) ran its first solo batch ~1-2 us slower
-        for _ in range(max(1, args.solo_warmup)):
-            solo.encode_batch_dev(sfr, sout, quality=args.quality)
-        solo.set_timing(1)
-        solo.reset_timing()
-        s0 = time.monotonic_ns()
-        for _ in range(args.solo_batches):
-            solo.encode_batch_dev(sfr, sout, quality=args.quality)
-        win = [s0, time.monotonic_ns()]
-        tm = solo.timing()
-        solo.close()
-        return tm, win
-
     if args.solo_batches > 0 and not args.no_kernel_events:
-        tm_solo, solo_win = solo_pass(set_size)
-        tm_solo1, solo1_win = solo_pass(1) if set_size > 1 else (tm_solo, solo_win)
+        PHASE("solo kernel timing")
+        tm_solo, solo_win = solo_timing(J, local, frames[:D], outd[:D], args, set_size)
+        tm_solo1, solo1_win = solo_timing(J, local, frames[:D], outd[:D], args, 1) if set_size > 1 else (tm_solo, solo_win)
 
     # Single-image latency on the drop-in path (main.cpp:29 -> Image::writeJPEG, one image
     # per call): jpge_encode_rgb8 on a 1-lane context, one frame per call, wall time per
     # call; device-in/device-out and pinned host-in/host-out (PCIe copies inside the call)
     latency = None
     if args.latency_calls > 0:
+        PHASE("latency calls")
         lat = J.Encoder(local, lanes=1)
         lat.set_subsampling(args.subsampling)
         hin = [torch.from_numpy(host[d].reshape(-1)).pin_memory() for d in range(min(D, 8))]
@@ -894,54 +1167,11 @@ def run_frames(args, rank, local, world, pg):
     # sampled it), averaged over the step's frames (frame i = input i mod D)
     syms = [int(enc.symbol_stats(host[d], quality=args.quality)[0].sum()) for d in range(D)]
     rec_bytes = 4.0 * sum(syms[i % D] for i in range(F)) / F
-    # per-kernel algorithmic bytes per launch; the entropy stage is two
-    # kernels: code (records -> the unstuffed bit stream) and pack (-> stuffed .jpg)
-    alg = {
-        "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
-        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 4 B each"),
-        "entropy_code_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + bit stream written (~.jpg size)"),
-        "entropy_pack_kernel": (2.0 * avg_jpeg, "bit stream read + stuffed .jpg bytes written"),
-    }
-    stage_alg = {"entropy_stage": (rec_bytes + avg_jpeg, "symbol records read 4 B each + .jpg bytes written")}
-    tm_key = {"fdct_kernel": "fdct_sum", "stats_kernel": "dc_stats_sum", "entropy_code_kernel": "code_sum",
-              "entropy_pack_kernel": "pack_sum", "entropy_stage": "entropy_sum"}
-    pmc_key = {"entropy_stage": "entropy_kernel"}
+    alg, stage_alg = alg_bytes(npx, cb, rec_bytes, avg_jpeg)
 
-    def rooflines(tm):
-        # per launch: a frame set's launch covers frames_per_launch frames (its bytes and
-        # its duration both); traffic (PMC, profiles/) is per frame
-        nl = max(1, tm.get("launches") or tm["frames"])
-        fpl = tm["frames"] / nl if tm["frames"] else 1.0
-        out = {}
-        timed = bool(tm.get("launches") or tm["frames"])
-        for name, (b, what) in list(alg.items()) + list(stage_alg.items()):
-            ms = tm[tm_key[name]] / nl
-            bl = b * fpl
-            tr = traffic.get(pmc_key.get(name, name))
-            if not timed or ms <= 0:  # (no launch of this pass was timed: no figure, not a zero)
-                out[name] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                             "traffic": int(tr * fpl) if tr else tr, "alg_bytes_per_launch": int(bl),
-                             "alg_bytes": what, "avg_kernel_ms": None, "timed_launches": 0,
-                             "reason": "no launch of this kernel was timed in this pass (kernel events off or "
-                                       "no sampled frame)"}
-                continue
-            ach = bl / (ms * 1e-3) / 1e9
-            out[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(tr * fpl) if tr else tr,
-                         "alg_bytes_per_launch": int(bl), "alg_bytes": what, "avg_kernel_ms": round(ms, 5),
-                         "timed_launches": nl, "frames_per_launch": round(fpl, 3)}
-        # the north star's "HBM-read roofline": K1's RGB8 read alone (3 B/px)
-        k1 = out["fdct_kernel"]
-        ms1 = tm["fdct_sum"] / nl
-        if ms1 > 0:
-            rd = 3.0 * npx * fpl / (ms1 * 1e-3) / 1e9
-            k1["read_achieved"] = round(rd, 1)
-            k1["read_frac"] = round(rd / HBM_PEAK_GBS, 4)
-        return out
-
-    stages = rooflines(tm)  # in situ: the timed region, lanes side by side (overlapping: diagnostic)
-    stages_solo = rooflines(tm_solo) if tm_solo else None
-    stages_solo1 = rooflines(tm_solo1) if tm_solo1 else None
+    stages = kernel_rooflines(tm, alg, stage_alg, traffic, npx)  # in situ (lanes overlap: diagnostic)
+    stages_solo = kernel_rooflines(tm_solo, alg, stage_alg, traffic, npx) if tm_solo else None
+    stages_solo1 = kernel_rooflines(tm_solo1, alg, stage_alg, traffic, npx) if tm_solo1 else None
     ms_step = dt_max / args.steps * 1e3
     # The headline roofline: the dominant kernel (longest exclusive time) ALONE on the GPU
     # (the solo pass), its duration from events bound to its own dispatch, so the figure
@@ -949,17 +1179,7 @@ def run_frames(args, rank, local, world, pg):
     # kernels overlap, so an in-situ duration is wall time shared with the other lanes.
     roofline = None
     if stages_solo:
-        dominant = max(alg, key=lambda k: stages_solo[k]["avg_kernel_ms"] or 0.0)
-        roofline = dict(kernel=dominant, timing="solo (1-lane encoder after the timed region; HIP events bound "
-                                                "to the kernel's dispatch, hipExtLaunchKernel)", **stages_solo[dominant])
-        # exclusive time of one launch x launches per step cannot exceed the step
-        lps = F / roofline["frames_per_launch"]
-        spent = lps * roofline["avg_kernel_ms"]
-        roofline["check"] = {"launches_per_step": round(lps, 1), "launches_x_avg_ms": round(spent, 3),
-                             "ms_per_step": round(ms_step, 3), "ok": spent <= ms_step}
-        if spent > ms_step:
-            raise SystemExit(f"bench: roofline check failed: {lps:.1f} launches x {roofline['avg_kernel_ms']} ms "
-                             f"= {spent:.3f} ms > {ms_step:.3f} ms per step")
+        roofline = solo_headline(stages_solo, alg, F, ms_step)
     elif stages["fdct_kernel"]["avg_kernel_ms"]:
         # no solo pass (--solo-batches 0): the in-situ figure, labelled as such (lanes
         # overlap, so it is shared wall time and carries no per-step check)
@@ -1021,7 +1241,8 @@ def run_frames(args, rank, local, world, pg):
             # CLOCK_MONOTONIC windows (rocprofv3 timestamps use the same clock): tools/rocprof_window.py
             "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win, "solo_single": solo1_win},
             # host CPU use over the timed region; quota throttling stalls the pipeline
-            "host_cpu": host_cpu_use(cg0, cg1, dt),
+            "host_cpu": host_cpu_use(cg0, cg1, dt, world),
+            "rank_cpus": [round(c, 2) for c in rank_cpus],
             "devices": args.devices,
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -1044,7 +1265,9 @@ def main(argv=None):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         device_plan(args.gpus, args.allow_shared_gpu)  # refuse before starting any rank
         sys.exit(spawn(args.gpus, argv))  # (the parent never touches a GPU)
-    rank, local, world, pg = dist_setup(args.gpus)
+    global PHASE
+    PHASE = PhaseWatch(args.phase_timeout)
+    rank, local, world, pg = dist_setup(args.gpus, args)
     args.devices = device_plan(world, args.allow_shared_gpu)
     run = {"4k-frames": run_frames, "batch1080": run_batch1080, "16k-striped": run_striped16k,
            "ppm-files": run_ppm_files, "dist-check": run_dist_check}[args.workload]

@@ -69,6 +69,8 @@ typedef struct {
     double code_sum, pack_sum; /* K3's entropy_code_kernel and entropy_pack_kernel alone (ms, accumulated) */
     uint64_t launches;         /* timed launches of each kernel (batches of small frames launch frame sets:
                                   one launch per kernel for up to 4 frames; the sums are per launch) */
+    uint64_t gate_timeouts;    /* single-frame calls whose table gate timed out on the device and were
+                                  re-coded ungated (jpge_encode_rgb8; not reset by jpge_reset_timing) */
 } jpge_timing;
 
 const char* jpge_strerror(int status);

@@ -99,7 +99,7 @@ class Timing(ctypes.Structure):
                 ("total", ctypes.c_float), ("fdct_sum", ctypes.c_double), ("dc_stats_sum", ctypes.c_double),
                 ("entropy_sum", ctypes.c_double), ("frames", ctypes.c_uint64),
                 ("symbols", ctypes.c_uint64), ("code_sum", ctypes.c_double), ("pack_sum", ctypes.c_double),
-                ("launches", ctypes.c_uint64)]
+                ("launches", ctypes.c_uint64), ("gate_timeouts", ctypes.c_uint64)]
 
 
 _LIB = None
@@ -454,7 +454,7 @@ class Encoder:
         return {"fdct": t.fdct, "dc_stats": t.dc_stats, "entropy": t.entropy, "total": t.total,
                 "fdct_sum": t.fdct_sum, "dc_stats_sum": t.dc_stats_sum, "entropy_sum": t.entropy_sum,
                 "frames": t.frames, "symbols": t.symbols, "code_sum": t.code_sum, "pack_sum": t.pack_sum,
-                "launches": t.launches}
+                "launches": t.launches, "gate_timeouts": t.gate_timeouts}
 
     def reset_timing(self) -> None:
         _check(lib().jpge_reset_timing(self._ctx), "reset_timing")

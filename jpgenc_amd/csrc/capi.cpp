@@ -4,6 +4,7 @@
 #include <pthread.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -24,9 +25,37 @@
 struct jpge_ctx {
     std::unique_ptr<jpge::Encoder> enc;
     std::unique_ptr<jpge::IngestBuffers, jpge::IngestBuffersDeleter> ingest;  // jpge_encode_files' buffers
+    // calls in flight, and the exit handler's release (live_release): a call that got in is
+    // waited for, every later one returns JPGE_E_ARG
+    std::mutex use_mu;
+    std::condition_variable use_cv;
+    int inflight = 0;
+    bool released = false;
 };
 
 namespace {
+// An entry point's use of a context: false for a null or released handle (or one without
+// an encoder); otherwise counted in flight until the call returns.
+class CtxUse {
+  public:
+    explicit CtxUse(jpge_ctx* c) : c_(c) {
+        if (!c_) return;
+        std::lock_guard<std::mutex> l(c_->use_mu);
+        if (c_->released || !c_->enc) { c_ = nullptr; return; }
+        ++c_->inflight;
+    }
+    ~CtxUse() {
+        if (!c_) return;
+        std::lock_guard<std::mutex> l(c_->use_mu);
+        if (--c_->inflight == 0) c_->use_cv.notify_all();
+    }
+    explicit operator bool() const { return c_ != nullptr; }
+    CtxUse(const CtxUse&) = delete;
+    CtxUse& operator=(const CtxUse&) = delete;
+
+  private:
+    jpge_ctx* c_;
+};
 jpge::FrameDesc frame(const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval) {
     jpge::FrameDesc f;
     f.rgb = rgb;
@@ -117,10 +146,12 @@ void live_mark_released(const void* h) {
 }
 void live_release(jpge_ctx* c) {
     live_remove(c);
-    if (c->enc) {  // wait for a call still running on another thread, then tear down
-        { std::lock_guard<std::recursive_mutex> wait(c->enc->call_mutex()); }
-        c->enc.reset();
+    {  // no call gets in from now on; the ones in flight are waited for, then tear down
+        std::unique_lock<std::mutex> l(c->use_mu);
+        c->released = true;
+        c->use_cv.wait(l, [&] { return c->inflight == 0; });
     }
+    c->enc.reset();
     c->ingest.reset();
     live_mark_released(c);
 }
@@ -180,13 +211,15 @@ int jpge_close(jpge_ctx* ctx) {
 }
 
 int jpge_set_timing(jpge_ctx* ctx, int every) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     ctx->enc->set_timing(every);
     return JPGE_OK;
 }
 
 int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
-    if (!ctx || !ctx->enc || !t) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !t) return JPGE_E_ARG;
     const auto& k = ctx->enc->times();
     t->fdct = k.fdct;
     t->dc_stats = k.dc_stats;
@@ -200,28 +233,33 @@ int jpge_get_timing(jpge_ctx* ctx, jpge_timing* t) {
     t->code_sum = k.code_sum;
     t->pack_sum = k.pack_sum;
     t->launches = k.launches;
+    t->gate_timeouts = ctx->enc->gate_timeouts();
     return JPGE_OK;
 }
 
 int jpge_reset_timing(jpge_ctx* ctx) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     ctx->enc->reset_timing();
     return JPGE_OK;
 }
 
 int jpge_get_lanes(jpge_ctx* ctx, int* lanes) {
-    if (!ctx || !ctx->enc || !lanes) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !lanes) return JPGE_E_ARG;
     *lanes = ctx->enc->lanes();
     return JPGE_OK;
 }
 
 int jpge_set_restart_interval(jpge_ctx* ctx, uint32_t mcus) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     return ctx->enc->set_restart(mcus) ? JPGE_E_ARG : JPGE_OK;
 }
 
 int jpge_set_subsampling(jpge_ctx* ctx, int mode) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     return ctx->enc->set_subsampling(mode) ? JPGE_E_ARG : JPGE_OK;
 }
 
@@ -236,7 +274,8 @@ int jpge_quality_tables(int quality, uint8_t qy[64], uint8_t qc[64]) {
 int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
                      const uint8_t qy[64], const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len,
                      uint32_t flags) {
-    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !out || !len) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !rgb || !qy || !qc || !out || !len) return JPGE_E_ARG;
     jpge::FrameDesc f = frame(rgb, w, h, stride, maxval);
     f.out = out;
     f.cap = cap;
@@ -247,7 +286,8 @@ int jpge_encode_rgb8(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, 
 
 int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy[64], const uint8_t qc[64],
                       uint32_t flags) {
-    if (!ctx || !ctx->enc || (!frames && n) || n < 0 || !qy || !qc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || (!frames && n) || n < 0 || !qy || !qc) return JPGE_E_ARG;
     std::vector<jpge::FrameDesc> fd(n);
     for (int i = 0; i < n; ++i) {
         fd[i] = frame(frames[i].rgb, frames[i].width, frames[i].height, frames[i].stride, frames[i].maxval);
@@ -265,14 +305,16 @@ int jpge_encode_batch(jpge_ctx* ctx, jpge_frame* frames, int n, const uint8_t qy
 int jpge_fdct_quant(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
                     const uint8_t qy[64], const uint8_t qc[64], int16_t* cy, int16_t* ccb, int16_t* ccr,
                     uint32_t flags) {
-    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !cy || !ccb || !ccr) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !rgb || !qy || !qc || !cy || !ccb || !ccr) return JPGE_E_ARG;
     return ctx->enc->fdct_quant(frame(rgb, w, h, stride, maxval), qy, qc, flags, cy, ccb, ccr);
 }
 
 int jpge_symbol_stats(jpge_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride, int maxval,
                       const uint8_t qy[64], const uint8_t qc[64], uint32_t counts[1024], uint64_t first[1024],
                       uint32_t flags) {
-    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !counts || !first) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !rgb || !qy || !qc || !counts || !first) return JPGE_E_ARG;
     return ctx->enc->symbol_stats(frame(rgb, w, h, stride, maxval), qy, qc, flags, counts, first);
 }
 
@@ -360,7 +402,8 @@ int jpge_parse_ppm(const uint8_t* buf, size_t n, uint8_t* rgb, size_t cap, uint3
 }
 
 int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, int quality) {
-    if (!ctx || !ctx->enc || !ppm_path || !jpg_path) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !ppm_path || !jpg_path) return JPGE_E_ARG;
     jpge::PpmImage img;
     int st = jpge::load_ppm_file(ppm_path, img);
     if (st) return st;
@@ -380,7 +423,8 @@ int jpge_encode_file(jpge_ctx* ctx, const char* ppm_path, const char* jpg_path, 
 
 int jpge_encode_files(jpge_ctx* ctx, const char* const* ppm_paths, const char* const* jpg_paths, int n, int quality,
                       size_t* lens, int* statuses, int group) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     return jpge::encode_files(*ctx->enc, ctx->ingest, ppm_paths, jpg_paths, n, quality, lens, statuses, group);
 }
 
@@ -401,7 +445,8 @@ static_assert(sizeof(jpge_stripe_summary) == sizeof(jpge::StripeSummary), "strip
 int jpge_stripe_transform(jpge_ctx* ctx, const uint8_t* rgb, size_t stride, uint32_t width, uint32_t height,
                           uint32_t mcu_row0, uint32_t mcu_rows, int maxval, const uint8_t qy[64],
                           const uint8_t qc[64], int32_t last_dc[3]) {
-    if (!ctx || !ctx->enc || !rgb || !qy || !qc || !last_dc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !rgb || !qy || !qc || !last_dc) return JPGE_E_ARG;
     jpge::Encoder::StripeDesc d;
     d.rgb = rgb;
     d.stride = stride;
@@ -414,13 +459,15 @@ int jpge_stripe_transform(jpge_ctx* ctx, const uint8_t* rgb, size_t stride, uint
 }
 
 int jpge_stripe_stats(jpge_ctx* ctx, const int32_t seed_dc[3], uint32_t counts[1024], uint64_t first[1024]) {
-    if (!ctx || !ctx->enc || !seed_dc || !counts || !first) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !seed_dc || !counts || !first) return JPGE_E_ARG;
     return ctx->enc->stripe_stats(seed_dc, counts, first);
 }
 
 int jpge_stripe_code(jpge_ctx* ctx, const uint32_t counts[1024], const uint64_t first[1024],
                      jpge_stripe_summary* summary, size_t* header_len) {
-    if (!ctx || !ctx->enc || !counts || !first || !summary) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !counts || !first || !summary) return JPGE_E_ARG;
     return ctx->enc->stripe_code(counts, first, reinterpret_cast<jpge::StripeSummary*>(summary), header_len);
 }
 
@@ -432,7 +479,8 @@ int jpge_stripe_place(const jpge_stripe_summary* all, int n, int index, size_t h
 
 int jpge_stripe_pack(jpge_ctx* ctx, const jpge_stripe_summary* all, int n, int index, uint8_t* out, size_t cap,
                      size_t* seg_off, size_t* seg_len, size_t* total_len) {
-    if (!ctx || !ctx->enc || !all || !out) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || !all || !out) return JPGE_E_ARG;
     return ctx->enc->stripe_pack(reinterpret_cast<const jpge::StripeSummary*>(all), n, index, out, cap, seg_off,
                                  seg_len, total_len);
 }
@@ -444,7 +492,8 @@ extern "C" {
 
 int jpge_color_convert(jpge_ctx* ctx, const double* in0, const double* in1, const double* in2, double* out0,
                        double* out1, double* out2, size_t n, int target, uint32_t flags) {
-    if (!ctx || !ctx->enc || (target != JPGE_TO_RGB && target != JPGE_TO_YCBCR)) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || (target != JPGE_TO_RGB && target != JPGE_TO_YCBCR)) return JPGE_E_ARG;
     const double* in[3] = {in0, in1, in2};
     double* out[3] = {out0, out1, out2};
     return ctx->enc->stage_color(in, out, n, target == JPGE_TO_YCBCR, flags);
@@ -452,7 +501,8 @@ int jpge_color_convert(jpge_ctx* ctx, const double* in0, const double* in1, cons
 
 int jpge_subsample_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int mode, double* out,
                          uint32_t* out_rows, uint32_t* out_cols, uint32_t flags) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     if (const int e = jpge::Encoder::subsample_shape(mode, rows, cols, out_rows, out_cols)) return e;
     if (!out) return JPGE_OK;
     return ctx->enc->stage_subsample(in, rows, cols, mode, out, flags);
@@ -460,20 +510,23 @@ int jpge_subsample_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_
 
 int jpge_dct_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, int dct_mode, double* out,
                    uint32_t flags) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     return ctx->enc->stage_dct(in, rows, cols, dct_mode, out, flags);
 }
 
 int jpge_quantize_plane(jpge_ctx* ctx, const double* in, uint32_t rows, uint32_t cols, const uint8_t table[64],
                         int32_t* out, uint32_t flags) {
-    if (!ctx || !ctx->enc) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use) return JPGE_E_ARG;
     return ctx->enc->stage_quantize(in, rows, cols, table, out, flags);
 }
 
 int jpge_encode_planes(jpge_ctx* ctx, const double* p0, const double* p1, const double* p2, uint32_t rows,
                        uint32_t cols, int colorspace, uint32_t real_width, uint32_t real_height, const uint8_t qy[64],
                        const uint8_t qc[64], uint8_t* out, size_t cap, size_t* len, uint32_t flags) {
-    if (!ctx || !ctx->enc || (colorspace != JPGE_TO_RGB && colorspace != JPGE_TO_YCBCR)) return JPGE_E_ARG;
+    CtxUse use(ctx);
+    if (!use || (colorspace != JPGE_TO_RGB && colorspace != JPGE_TO_YCBCR)) return JPGE_E_ARG;
     const double* p[3] = {p0, p1, p2};
     return ctx->enc->encode_planes(p, rows, cols, colorspace == JPGE_TO_YCBCR, real_width, real_height, qy, qc, out,
                                    cap, len, flags);

@@ -457,6 +457,12 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     e->lat_prof_ = env_int("JPGE_LAT_PROF", 0, 0, 1) != 0;
     e->table_helper_ = env_int("JPGE_TABLE_HELPER", 1, 0, 1) != 0;
     e->gate_ = env_int("JPGE_GATE", 1, 0, 2);
+    // Launch-serialising debug modes block the host in a launch until the kernel (or its
+    // predecessor) has finished, so the host could never open the gate behind the gate
+    // kernel: every call would run into its time-out.  They get the ungated path.
+    if (env_int("AMD_SERIALIZE_KERNEL", 0, 0, 3) != 0 || env_int("HIP_LAUNCH_BLOCKING", 0, 0, 1) != 0) e->gate_ = 0;
+    if (const int us = env_int("JPGE_TEST_GATE_TIMEOUT_US", 0, 0, 1000000)) e->gate_ticks_ = 100ull * (uint64_t)us;
+    e->gate_delay_us_ = env_int("JPGE_TEST_GATE_DELAY_US", 0, 0, 1000000);
     if (e->gate_ == 2) {  // (the runtime's stream wait needs device support)
         int wv = 0;
         if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess || !wv) e->gate_ = 0;
@@ -540,6 +546,8 @@ int Encoder::add_slots(Lane& ln, int count) {
         std::memset(s->h_result, 0, 64);
         JPGE_HIP(hipHostGetDevicePointer((void**)&s->d_result_host, s->h_result, 0));
         JPGE_HIP(hipMalloc((void**)&s->d_tab, kTabBytes + kHdrMax));
+        // (zeroed too: a gate that times out leaves the code kernel these tables)
+        JPGE_HIP(hipMemset(s->d_tab, 0, kTabBytes + kHdrMax));
         ln.slots.push_back(std::move(s));
     }
     return kOk;
@@ -864,7 +872,10 @@ int Encoder::phase1_set(Slot* const* s, int n, const FdctArgs* a_in, const Stats
 // build the four tables (generateHuffmanCode semantics, Huffman.cpp:3-35) and the
 // headers into the slot's pinned staging buffer.
 int Encoder::build_tables(Slot& s, bool parallel, TableHelper* helper) {
-    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ ? nap_us_ : (parallel ? 0 : hist_nap_us_), &s.export_queued,
+    // (frames above kFirstSleepMaxPixels nap even on a single lane: their kernels take
+    // milliseconds, and a spinning thread would burn a core for them)
+    const bool big = (uint64_t)s.g.width * s.g.height > kFirstSleepMaxPixels;
+    if (const int w = wait_seq(&s.h_hist->seq, s.seq, s.stream, nap_ || big ? nap_us_ : (parallel ? 0 : hist_nap_us_), &s.export_queued,
                                s.inline_tables ? s.guess_hist : nullptr))
         return w;
     if (lat_prof_) lat_hist_seen_ = std::chrono::steady_clock::now();
@@ -981,7 +992,8 @@ int Encoder::finish(Slot& s, FrameDesc& f, uint32_t flags, bool guess_wait, cons
     // and their short waits would blur the estimate of the real one)
     WaitGuess* const guess =
         guess_wait && (uint64_t)s.g.width * s.g.height <= kFirstSleepMaxPixels ? s.guess_result : nullptr;
-    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ ? nap_us_ : 0, nullptr, guess, idle)) return w;
+    const bool big = (uint64_t)s.g.width * s.g.height > kFirstSleepMaxPixels;  // (as build_tables)
+    if (const int w = wait_seq(&s.h_result[3], s.seq, s.stream, nap_ || big ? nap_us_ : 0, nullptr, guess, idle)) return w;
     if (s.timed) {
         JPGE_HIP(wait_event(s.ev[7]));
         std::lock_guard<std::mutex> g(times_mu_);
@@ -1049,7 +1061,8 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (!st && gate_ == 1) {  // a workgroup of ours waits and copies (entropy.hip gate_copy_kernel)
         s.h_result[2] = 0;  // (its time-out flag)
         if (launch_gate_copy(reinterpret_cast<const uint32_t*>(s.d_result_host + 6), gate.value, s.d_tab_host, s.d_tab,
-                             (uint32_t)((kTabBytes + kHdrMax) / 16), s.d_result_host + 2, s.stream) == hipSuccess) {
+                             (uint32_t)((kTabBytes + kHdrMax) / 16), s.d_result_host + 2, gate_ticks_,
+                             s.stream) == hipSuccess) {
             gate.shut = true;
             st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/1);
             if (st) gate.open();
@@ -1071,9 +1084,12 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (lat_prof_) T[1] = clk::now();
     // The tables: on this thread, with the helper thread of a 1-lane encoder for frames
     // of 1 MPix and up (armed now, so its wake-up overlaps the kernels; spawning threads
-    // per call would cost more than the tables it overlaps)
+    // per call would cost more than the tables it overlaps).  Not above
+    // kFirstSleepMaxPixels: the helper spins from here to the histograms, which take
+    // milliseconds there, for tables that are a small part of such a call.
     TableHelper* helper = nullptr;
-    if (!st && table_helper_ && lanes_.size() == 1 && (uint64_t)f.width * f.height >= (1u << 20)) {
+    const uint64_t npx = (uint64_t)f.width * f.height;
+    if (!st && table_helper_ && lanes_.size() == 1 && npx >= (1u << 20) && npx <= kFirstSleepMaxPixels) {
         if (!helper_) helper_.reset(new TableHelper());
         helper = helper_.get();
         helper->arm();
@@ -1081,7 +1097,9 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     if (!st) st = build_tables(s, false, helper);
     if (helper) helper->disarm();
     if (lat_prof_) T[2] = clk::now();
+    const bool gated = gate.shut;
     if (gate.shut) {
+        if (gate_delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(gate_delay_us_));  // (tests)
         gate.open();
         if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true, /*parts=*/2);
     } else {
@@ -1090,6 +1108,17 @@ int Encoder::encode(FrameDesc& f, const uint8_t qy[64], const uint8_t qc[64], ui
     }
     if (lat_prof_) T[3] = clk::now();
     if (!st) st = finish(s, f, flags);
+    if (st == kErrTimeout && gated && s.h_result[2] == 1) {
+        // The gate kernel timed out before the host opened it (a host thread stalled for
+        // longer than the time-out): the code kernel ran on stale tables, so the frame is
+        // coded again behind a plain copy of the tables now in h_tab.
+        gate_timeouts_.fetch_add(1, std::memory_order_relaxed);
+        s.h_result[2] = 0;
+        s.seq = ++seq_counter_;
+        st = import_tables_copy(s);
+        if (!st) st = launch_entropy_phase(s, nullptr, /*lone=*/true);
+        if (!st) st = finish(s, f, flags);
+    }
     if (lat_prof_) T[4] = clk::now();
     // Every output byte is in place.  Device output on a 1-lane encoder: the result word is
     // written once every pack workgroup's (write-through) stores have completed, so the

@@ -171,6 +171,12 @@ class Encoder {
     bool table_helper_ = true;             // JPGE_TABLE_HELPER=0: none
     int gate_ = 1;  // encode()'s gate: 1 our wait-and-copy kernel, 2 the runtime's stream wait (JPGE_GATE), 0 none
     uint32_t gate_count_ = 0;  // gated calls (their gate values: 1, 2, ...)
+    uint64_t gate_ticks_ = 100000000ull;  // the gate kernel's time-out (1 s; JPGE_TEST_GATE_TIMEOUT_US, tests)
+    int gate_delay_us_ = 0;               // JPGE_TEST_GATE_DELAY_US (tests): the host opens the gate this late
+    std::atomic<uint64_t> gate_timeouts_{0};  // calls re-coded after a gate time-out
+  public:
+    uint64_t gate_timeouts() const { return gate_timeouts_.load(std::memory_order_relaxed); }
+  private:
     uint32_t entropy_wgs_ = 0;  // JPGE_ENTROPY_WGS: entropy workgroup count (tests; clamped)
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)

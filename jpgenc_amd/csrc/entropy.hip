@@ -893,16 +893,16 @@ SegLayout seg_layout(const Geometry& g, uint32_t restart_mcus, uint32_t wgs_over
 // time-out (~1 s) ends the wait whatever happens and flags the frame's result word
 // (host_result[2]), so the call fails instead of coding with stale tables.
 constexpr uint32_t kGateThreads = 512;
-constexpr uint64_t kGateTimeoutTicks = 100000000ull;  // s_memrealtime runs at 100 MHz
 __global__ __launch_bounds__(kGateThreads) void gate_copy_kernel(const uint32_t* gate, uint32_t value, const uint4* src,
-                                                                 uint4* dst, uint32_t n16, uint64_t* fail) {
+                                                                 uint4* dst, uint32_t n16, uint64_t* fail,
+                                                                 uint64_t timeout_ticks) {
     __shared__ uint32_t open;
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t o = 1;
         while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
             __builtin_amdgcn_s_sleep(4);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {  // (s_memrealtime: 100 MHz)
                 o = 0;
                 break;
             }
@@ -919,9 +919,9 @@ __global__ __launch_bounds__(kGateThreads) void gate_copy_kernel(const uint32_t*
 }
 
 hipError_t launch_gate_copy(const uint32_t* gate, uint32_t value, const void* src, void* dst, uint32_t n16,
-                            uint64_t* fail, hipStream_t s) {
+                            uint64_t* fail, uint64_t timeout_ticks, hipStream_t s) {
     hipLaunchKernelGGL(gate_copy_kernel, dim3(1), dim3(kGateThreads), 0, s, gate, value,
-                       reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16, fail);
+                       reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16, fail, timeout_ticks);
     return hipGetLastError();
 }
 

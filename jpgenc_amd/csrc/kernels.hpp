@@ -374,11 +374,11 @@ hipError_t launch_entropy(const EntropyArgs& a, hipStream_t s, const KTimer* cod
 // its two halves: the code kernel does not read hdr_len, so it can be queued before the
 // header is known (encoder.cpp, encode()'s gate); the pack kernel (and placement)
 hipError_t launch_entropy_code(const EntropyArgs& a, hipStream_t s, const KTimer* code = nullptr);
-// encode()'s gate: wait (one workgroup, ~1 s at most, then *fail = 1) until *gate == value
-// (mapped host memory), then copy n16 16-byte units src -> dst (src: device view of mapped
-// host memory)
+// encode()'s gate: wait (one workgroup, at most timeout_ticks of the 100 MHz realtime
+// counter, then *fail = 1 and no copy) until *gate == value (mapped host memory), then copy
+// n16 16-byte units src -> dst (src: device view of mapped host memory)
 hipError_t launch_gate_copy(const uint32_t* gate, uint32_t value, const void* src, void* dst, uint32_t n16,
-                            uint64_t* fail, hipStream_t s);
+                            uint64_t* fail, uint64_t timeout_ticks, hipStream_t s);
 hipError_t launch_entropy_pack(const EntropyArgs& a, hipStream_t s, const KTimer* pack = nullptr);
 // stripes: code kernel + summary scan; then placement scan + pack kernel
 hipError_t launch_entropy_code_summary(const EntropyArgs& a, hipStream_t s);

@@ -55,7 +55,7 @@ class BatchGather:
         self.last = 0
         self.got = [None, None]    # rank 0: every rank's lengths of the batch in buffer b
         self.where = [None, None]  # rank 0: frame offsets in batch[b] (built on first use)
-        self._ptrs = {}            # id(segment list) -> (the list, its device pointers as a ctypes array)
+        self._ptrs = {}            # the segments' device pointers (tuple) -> the same as a ctypes array (<= 4 kept)
         self.dev_index = torch.device(device).index if self.cuda else None
         if self.cuda and self.dev_index is None:
             self.dev_index = torch.cuda.current_device()
@@ -139,11 +139,16 @@ class BatchGather:
         if total and self.cuda:
             from . import concat_segments
 
-            key = id(segments)
-            hit = self._ptrs.get(key)
-            if hit is None or hit[0] is not segments:
-                hit = self._ptrs[key] = (segments, (ctypes.c_void_p * len(segments))(*[t.data_ptr() for t in segments]))
-            concat_segments(self.dev_index, torch.cuda.current_stream().cuda_stream, hit[1],
+            # (keyed by the pointers themselves, not the list object: a list reused with a
+            # tensor replaced must not hand the kernel stale pointers; bounded, so
+            # fresh lists per post do not pin old segments)
+            key = tuple(t.data_ptr() for t in segments)
+            arr = self._ptrs.get(key)
+            if arr is None:
+                if len(self._ptrs) >= 4:
+                    self._ptrs.pop(next(iter(self._ptrs)))
+                arr = self._ptrs[key] = (ctypes.c_void_p * len(key))(*key)
+            concat_segments(self.dev_index, torch.cuda.current_stream().cuda_stream, arr,
                             (ctypes.c_size_t * len(lens))(*lens), run.data_ptr())
         elif total:
             torch.cat([seg[:n] for seg, n in zip(segments, lens) if n], out=run)

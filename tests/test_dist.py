@@ -2,6 +2,7 @@
 frames (distinct seeds, weak scaling, no data-path collective); the process group
 only provides barriers, the max-over-ranks time and the sum of pixels."""
 import os
+import time
 import socket
 import sys
 
@@ -116,6 +117,36 @@ def test_bench_spawn_propagates_a_failing_rank():
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 3
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.timeout(150)
+def test_bench_phase_watchdog_names_a_stuck_rank():
+    """A rank stuck in one phase (a first 8-GPU run that stalls in RCCL
+    setup or a transfer) exits with status 124 once the phase outlives --phase-timeout, and
+    says which rank and phase; the launcher ends the others and returns that status."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["JPGE_BENCH_HANG_RANK"] = "1"  # rank 1 sleeps inside a named phase; rank 0 waits in a barrier
+    env["JPGE_BENCH_DEVICE_COUNT"] = "2"
+    t = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "dist-check",
+                        "--phase-timeout", "4", "--pg-timeout", "60"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 124, r.stderr[-2000:]
+    assert "rank 1: phase 'dist-check: stuck (test hook)' exceeded its 4 s limit" in r.stderr
+    assert time.monotonic() - t < 60
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_records_the_cgroup_quota():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    q = bench.cgroup_quota_cpus()
+    assert q is None or q > 0
+    h = bench.host_cpu_use({"usage_usec": 0}, {"usage_usec": 4_000_000}, 2.0, 2)
+    assert h["cpus_used"] == 2.0 and h["cpus_per_rank"] == 1.0 and "quota_cpus" in h
 
 
 def test_batch_share_deals_every_frame_once():

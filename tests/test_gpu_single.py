@@ -82,3 +82,58 @@ def test_gate_modes_same_bytes(monkeypatch, mode):
             assert enc.encode(rgb, quality=q) == _oracle.encode(rgb, q)
     finally:
         enc.close()
+
+
+def test_gate_timeout_recodes(monkeypatch):
+    """The gate kernel's time-out path: the device waits at
+    most 300 us for the gate, the host opens it 30 ms after building the tables, so every
+    call's gate times out and its code kernel runs on the previous call's tables (zeros for
+    the first).  The call must notice (the gate's fail word), code the frame again behind a
+    plain copy of the tables, and return the oracle's bytes; the context keeps working."""
+    import torch
+
+    monkeypatch.setenv("JPGE_TEST_GATE_TIMEOUT_US", "300")
+    monkeypatch.setenv("JPGE_TEST_GATE_DELAY_US", "30000")
+    enc = J.Encoder(0, lanes=1)
+    monkeypatch.delenv("JPGE_TEST_GATE_TIMEOUT_US")
+    monkeypatch.delenv("JPGE_TEST_GATE_DELAY_US")
+    try:
+        cases = [(1920, 1080, 90), (200, 136, 50), (640, 480, 100), (1920, 1080, 90)]
+        for k, (w, h, q) in enumerate(cases):
+            rgb = J.synth_rgb8(131 + k, w, h)
+            assert enc.encode(rgb, quality=q) == _oracle.encode(rgb, q)
+        w, h = 1280, 720
+        rgb = J.synth_rgb8(7, w, h)
+        d_in = torch.from_numpy(rgb.reshape(-1)).cuda()
+        cap = J.max_jpeg_bytes(w, h)
+        out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        n = enc.encode_ptr(d_in.data_ptr(), w, h, w * 3, out.data_ptr(), cap, quality=90)
+        assert out[:n].cpu().numpy().tobytes() == _oracle.encode(rgb, 90)
+        # every call ran into the time-out (frames >= 1 MPix build tables with the helper
+        # thread; all of them open the gate 30 ms late)
+        assert enc.timing()["gate_timeouts"] == len(cases) + 1
+    finally:
+        enc.close()
+    plain = J.Encoder(0, lanes=1)  # (no hooks: the gate opens in time)
+    try:
+        rgb = J.synth_rgb8(8, 1920, 1080)
+        assert plain.encode(rgb, quality=90) == _oracle.encode(rgb, 90)
+        assert plain.timing()["gate_timeouts"] == 0
+    finally:
+        plain.close()
+
+
+def test_serialised_launches_skip_the_gate(monkeypatch):
+    """AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING block the host in each launch until the
+    kernel ends, so a gated call could never open its gate in time: such a context takes
+    the ungated path (no time-outs, the same bytes).  The runtime reads these variables at
+    its own start, so here only the library's reaction is checked."""
+    monkeypatch.setenv("AMD_SERIALIZE_KERNEL", "3")
+    enc = J.Encoder(0, lanes=1)
+    monkeypatch.delenv("AMD_SERIALIZE_KERNEL")
+    try:
+        rgb = J.synth_rgb8(9, 1920, 1080)
+        assert enc.encode(rgb, quality=90) == _oracle.encode(rgb, 90)
+        assert enc.timing()["gate_timeouts"] == 0
+    finally:
+        enc.close()
