@@ -710,7 +710,23 @@ def run_striped16k(args, rank, local, world, pg):
     roofline = stages_solo = None
     solo_win = None
     hs = 16 * nr if world > 1 else H
-    if args.solo_batches > 0 and not args.no_kernel_events:
+    # the output against the oracle's hash of this configuration (tests/golden/large_frames.json)
+    verified = None
+    if rank == 0 and not args.no_verify:
+        PHASE("verification")
+        with open(os.path.join(ROOT, "tests", "golden", "large_frames.json")) as f:
+            gold = [g for g in json.load(f)["frames"] if (g["width"], g["height"], g["seed"], g["quality"],
+                                                          g.get("restart", 0)) == (W, H, 5, args.quality, restart)]
+        if gold:
+            got = hashlib.sha256(out[:n].cpu().numpy().tobytes()).hexdigest()
+            verified = {"sha256_match": got == gold[0]["sha256"] and int(n) == gold[0]["len"],
+                        "method": "sha256 of the last step's .jpg (gathered on rank 0) against the oracle's "
+                                  "(tests/golden/large_frames.json)"}
+            if not verified["sha256_match"]:
+                raise SystemExit(f"16k-striped: output differs from the oracle's ({got} vs {gold[0]['sha256']})")
+        else:
+            verified = {"sha256_match": None, "method": "no oracle hash recorded for this quality/restart"}
+    if args.solo_batches > 0 and not args.no_kernel_events and rank == 0:
         PHASE("solo kernel timing")
         enc.close()
         tm_solo, solo_win = solo_timing(J, local, [(src.data_ptr(), W, hs, W * 3)], [(out.data_ptr(), cap)], args, 1,
@@ -755,6 +771,7 @@ def run_striped16k(args, rank, local, world, pg):
             if stages_solo else None,
             "stages_solo": stages_solo,
             "solo_rows": hs,
+            "verified": verified,
             "host_cpu": host_cpu_use(cg0, cg1, dt, world),
             "rank_cpus": [round(c, 2) for c in rank_cpus],
             "windows_monotonic_ns": {"timed": [win0, win1], "solo": solo_win},
@@ -946,7 +963,7 @@ def run_batch1080(args, rank, local, world, pg):
     ms_step = dt_max / args.steps * 1e3
     stages_solo = stages_solo1 = roofline = None
     solo_win = solo1_win = None
-    if args.solo_batches > 0 and not args.no_kernel_events and share:
+    if args.solo_batches > 0 and not args.no_kernel_events and share and rank == 0:
         PHASE("solo kernel timing")
         sfr = frames[:min(len(frames), 32)]
         sout = outd[0][:len(sfr)]
@@ -1116,7 +1133,8 @@ def run_frames(args, rank, local, world, pg):
     tm_solo = tm_solo1 = None
     solo_win = solo1_win = None
     set_size = max(1, min(4, (4 * 3840 * 2160) // (W * H))) if D >= 2 else 1
-    if args.solo_batches > 0 and not args.no_kernel_events:
+    # (rank 0 only: the other ranks' kernels would share its GPU in a shared-GPU rehearsal)
+    if args.solo_batches > 0 and not args.no_kernel_events and rank == 0:
         PHASE("solo kernel timing")
         tm_solo, solo_win = solo_timing(J, local, frames[:D], outd[:D], args, set_size)
         tm_solo1, solo1_win = solo_timing(J, local, frames[:D], outd[:D], args, 1) if set_size > 1 else (tm_solo, solo_win)
@@ -1125,7 +1143,7 @@ def run_frames(args, rank, local, world, pg):
     # per call): jpge_encode_rgb8 on a 1-lane context, one frame per call, wall time per
     # call; device-in/device-out and pinned host-in/host-out (PCIe copies inside the call)
     latency = None
-    if args.latency_calls > 0:
+    if args.latency_calls > 0 and rank == 0:
         PHASE("latency calls")
         lat = J.Encoder(local, lanes=1)
         lat.set_subsampling(args.subsampling)
@@ -1165,8 +1183,8 @@ def run_frames(args, rank, local, world, pg):
     # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3;
     # the count per frame from every distinct input's histograms (whether or not a pass
     # sampled it), averaged over the step's frames (frame i = input i mod D)
-    syms = [int(enc.symbol_stats(host[d], quality=args.quality)[0].sum()) for d in range(D)]
-    rec_bytes = 4.0 * sum(syms[i % D] for i in range(F)) / F
+    syms = [int(enc.symbol_stats(host[d], quality=args.quality)[0].sum()) for d in range(D)] if rank == 0 else [0]
+    rec_bytes = 4.0 * sum(syms[i % len(syms)] for i in range(F)) / F
     alg, stage_alg = alg_bytes(npx, cb, rec_bytes, avg_jpeg)
 
     stages = kernel_rooflines(tm, alg, stage_alg, traffic, npx)  # in situ (lanes overlap: diagnostic)

@@ -1,6 +1,6 @@
 // K3 entropy coding (gfx950): Huffman emission (Image.cpp:737-829) in MCU
 // interleave order (Image.cpp:957-968), 1-fill and 0xFF00 stuffing
-// (BitstreamGeneric.hpp:213-248), EOI (Image.cpp:1003-1005).  Two launches:
+// (BitstreamGeneric.hpp:213-248), EOI (Image.cpp:972).  Two launches:
 //
 // entropy_code_kernel — G persistent workgroups; workgroup w owns the contiguous
 //   tiles [w*T/G, (w+1)*T/G) of 128 blocks (2..kEntropyMaxTilesPerWg tiles).
@@ -801,7 +801,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
     if (last && tid == 0) {
         uint64_t len = 0;  // end of the image (EOI written) or of the stripe's bytes
         if (fits) {
-            if (eoi) {  // EOI, Image.cpp:1003-1005
+            if (eoi) {  // EOI, Image.cpp:972
                 uint8_t* const m = a.out + d;
                 const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(m, 0, 2, 0x00020000);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0xFF, mrs, 0, 0, kPackStoreAux);

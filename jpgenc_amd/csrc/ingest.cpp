@@ -1,6 +1,6 @@
 // PPM files -> .jpg files, pipelined (the PPM ingest + H2D
 // pipeline).  Replaces a loop of the reference's main.cpp:8-32 (loadPPM +
-// writeJPEG per file, Image.cpp:421-538 / 831-1006) over many files.
+// writeJPEG per file, Image.cpp:421-538 / 831-976) over many files.
 //
 // Three stages run side by side on groups of frames:
 //   read   — worker threads read each file straight into pinned host memory and

@@ -611,7 +611,7 @@ void emit_block(BitWriter& bw, const std::vector<Sym>& s, const Table& dc, const
     }
 }
 
-// restart = 0: writeJPEG (Image.cpp:831-1006).  restart = R > 0: the restart-interval
+// restart = 0: writeJPEG (Image.cpp:831-976).  restart = R > 0: the restart-interval
 // variant — DC chains reset per interval, and after every interval but the last the
 // stream is 1-filled, stuffed and followed by RSTn (n = interval index mod 8).
 // s444: the S444 variant (run_to_quant444; Y 1x1 in SOF0; MCU = Y, Cb, Cr).
