@@ -44,7 +44,7 @@ def main():
                                                  for i in range(0, len(v), 32)) + ")"
             print(f"   {n:28s} n={len(v):5d} mean {sum(v) / len(v) / 1e3:8.2f} us  median "
                   f"{statistics.median(v) / 1e3:8.2f} us{extra}")
-        ev = {"timed": b["stages"], "solo": b.get("stages_solo"),
+        ev = {"timed": b.get("stages"), "solo": b.get("stages_solo"),
               "solo_single": b.get("stages_solo_single_frame")}[label] or {}
         for k, v in ev.items():
             if v.get("avg_kernel_ms") is None:

@@ -12,6 +12,9 @@
 #           config 4 (batch1080) on one rank and on 2 ranks sharing the GPU
 #                                                                     -> gpurun_out/rp/b1080{,x2}.json
 #           16384^2 frames through the pipeline                       -> gpurun_out/rp/16k.json
+#           config 5 (16k-striped, restart per MCU row) on one GPU    -> gpurun_out/rp/16ks.json
+#           rocprofv3 --kernel-trace --stats of the batch1080 and 16k-striped lines, with
+#             their solo windows next to the lines' roofline events   -> gpurun_out/rp/{trace_b1080,trace_16ks}/, window_*.txt
 #   tools/round_profiles.sh A|B
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -49,6 +52,15 @@ B)
   line $O/b1080x2.json
   timeout -k 10 300 python3 bench.py --width 16384 --height 16384 --frames 16 --steps 5 --warmup 1 --no-cpu-baseline --latency-calls 0 > $O/16k.json 2> $O/16k.err || { tail -5 $O/16k.err; exit 1; }
   line $O/16k.json
+  timeout -k 10 300 python3 bench.py --workload 16k-striped > $O/16ks.json 2> $O/16ks.err || { tail -5 $O/16ks.err; exit 1; }
+  line $O/16ks.json
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_b1080 -o run -- \
+    python3 bench.py --workload batch1080 --no-cpu-baseline --steps 10 > $O/prof_b1080.json 2> $O/prof_b1080.err || { tail -5 $O/prof_b1080.err; exit 1; }
+  python3 tools/rocprof_window.py $O/trace_b1080 $O/prof_b1080.json | tee $O/window_b1080.txt
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_16ks -o run -- \
+    python3 bench.py --workload 16k-striped --no-cpu-baseline --steps 10 > $O/prof_16ks.json 2> $O/prof_16ks.err || { tail -5 $O/prof_16ks.err; exit 1; }
+  python3 tools/rocprof_window.py $O/trace_16ks $O/prof_16ks.json | tee $O/window_16ks.txt
+  find $O/trace_b1080 $O/trace_16ks -name '*kernel_trace.csv' -exec gzip -9 {} + 2>/dev/null
   ;;
 esac
 true
