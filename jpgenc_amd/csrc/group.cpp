@@ -296,7 +296,11 @@ int jpge_group_encode_striped(jpge_group* g, const uint8_t* rgb, uint32_t width,
         if (int e = g->grow(m, g->rgb, g->rgb_cap, (size_t)(y1 - y0) * row)) return e;
         if (int e = g->grow(m, g->out, g->out_cap, file_cap)) return e;
         GRP_HIP(hipSetDevice(g->dev[m]));
-        GRP_HIP(hipMemcpy2D(g->rgb[m], row, rgb + (size_t)y0 * pitch, pitch, row, y1 - y0, hipMemcpyHostToDevice));
+        // (on the member's stream: the null stream would slow every later launch on the
+        // members' lane streams)
+        GRP_HIP(hipMemcpy2DAsync(g->rgb[m], row, rgb + (size_t)y0 * pitch, pitch, row, y1 - y0, hipMemcpyHostToDevice,
+                                 g->xs[m]));
+        GRP_HIP(hipStreamSynchronize(g->xs[m]));
         return (int)JPGE_OK;
     });
     if (st) return st;
@@ -415,7 +419,8 @@ int jpge_group_encode_striped(jpge_group* g, const uint8_t* rgb, uint32_t width,
         GRP_HIP(hipStreamSynchronize(g->xs[0]));
     }
     GRP_HIP(hipSetDevice(g->dev[0]));
-    GRP_HIP(hipMemcpy(out, g->out[0], tot, hipMemcpyDeviceToHost));
+    GRP_HIP(hipMemcpyAsync(out, g->out[0], tot, hipMemcpyDeviceToHost, g->xs[0]));
+    GRP_HIP(hipStreamSynchronize(g->xs[0]));
     *len = tot;
     return (int)JPGE_OK;
 }

@@ -118,6 +118,17 @@ struct IngestBuffers {
     PinnedBuf pin[2][64];   // file bytes (then the frame) of each group's frames
     DevBuf dout[2][64];     // .jpg bytes in device memory
     PinnedBuf hout[2][64];  // .jpg bytes on the way to the file
+    // the writers' device-to-host copies, one non-blocking stream per writer thread: never
+    // the null stream, whose use slows every later launch on the encoder's lane streams
+    hipStream_t copy[64] = {};
+    hipStream_t stream(int t) {
+        if (!copy[t] && hipStreamCreateWithFlags(&copy[t], hipStreamNonBlocking) != hipSuccess) copy[t] = nullptr;
+        return copy[t];
+    }
+    ~IngestBuffers() {
+        for (hipStream_t s : copy)
+            if (s) hipStreamDestroy(s);
+    }
 };
 void IngestBuffersDeleter::operator()(IngestBuffers* b) const { delete b; }
 
@@ -160,20 +171,24 @@ int encode_files(Encoder& enc, std::unique_ptr<IngestBuffers, IngestBuffersDelet
         const double t0 = ms();
         const int s = g & 1, i0 = g * B, cnt = std::min(B, n - i0);
         std::atomic<int> next{0};
-        auto work = [&] {
+        const int nw = std::min(readers, cnt);
+        for (int t = 0; t < nw; ++t) bufs->stream(t);  // (created here, on one thread)
+        auto work = [&](int t) {
             hipSetDevice(device);
+            hipStream_t cs = bufs->copy[t];
             for (int k; (k = next.fetch_add(1)) < cnt;) {
                 const int i = i0 + k;
                 if (status[i]) continue;
-                int st = hout[s][k].reserve(length[i]);
-                if (!st && hipMemcpy(hout[s][k].p, dout[s][k].p, length[i], hipMemcpyDeviceToHost) != hipSuccess)
+                int st = cs ? hout[s][k].reserve(length[i]) : kErrHip;
+                if (!st && (hipMemcpyAsync(hout[s][k].p, dout[s][k].p, length[i], hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                            hipStreamSynchronize(cs) != hipSuccess))
                     st = kErrHip;
                 status[i] = st ? st : write_file(out[i], hout[s][k].p, length[i]);
             }
         };
         std::vector<std::thread> th;
-        for (int t = 1; t < std::min(readers, cnt); ++t) th.emplace_back(work);
-        work();
+        for (int t = 1; t < nw; ++t) th.emplace_back(work, t);
+        work(0);
         for (auto& t : th) t.join();
         if (trace) std::fprintf(stderr, "ingest g%d write %.2f .. %.2f ms\n", g, t0, ms());
     };

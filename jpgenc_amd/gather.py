@@ -75,6 +75,16 @@ class BatchGather:
         # p2p senders pack into a buffer of their own (rank 0 packs into its region directly)
         self.packed = [torch.empty(cap_bytes if (rank and self.transport == "p2p") else 1, dtype=torch.uint8,
                                    device=device) for _ in range(2)]
+        # every GPU operation of the gather (the concat launch, its events, the RCCL calls'
+        # stream waits) runs on a stream of its own, never the null stream: an operation
+        # there makes every later launch on the encoder's lane streams slower (the 4K
+        # pipeline lost 3.5% to one memset)
+        self.side = torch.cuda.Stream(device=self.dev_index) if self.cuda else None
+
+    def _on_side(self):
+        import contextlib
+
+        return self.torch.cuda.stream(self.side) if self.side is not None else contextlib.nullcontext()
 
     def _open_ipc(self):
         """Every rank opens rank 0's two batch buffers (HIP IPC).  The handles travel over
@@ -112,6 +122,10 @@ class BatchGather:
     def post(self, segments, lens) -> None:
         """segments: this rank's frames' byte tensors (length >= lens[k] each), in share
         order, from the set acquire() named; lens: their .jpg lengths (host ints)."""
+        with self._on_side():
+            self._post(segments, lens)
+
+    def _post(self, segments, lens) -> None:
         torch, dist = self.torch, self.dist
         b = self.turn
         self.turn ^= 1
@@ -200,6 +214,10 @@ class BatchGather:
     def wait(self) -> None:
         """Every posted transfer complete (rank 0: `batch` holds the last batch once every
         rank has returned from wait(), e.g. after a barrier)."""
+        with self._on_side():
+            self._wait()
+
+    def _wait(self) -> None:
         for b in (self.last ^ 1, self.last):  # (the older batch's receives first, as they were posted)
             if self.rank == 0:
                 self._complete(b)

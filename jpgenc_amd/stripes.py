@@ -88,7 +88,28 @@ def encode_stripe_dist(enc, rgb_ptr: int, stride: int, width: int, height: int, 
     0's `out` holds the whole file; returns its length (every rank).  restart: the
     encoder's restart interval (enc.set_restart), whose boundaries include every
     stripe start — then there is no DC seed exchange and the summaries only place
-    byte runs (the RCCL traffic is the histogram all-reduce and the segment gather)."""
+    byte runs (the RCCL traffic is the histogram all-reduce and the segment gather).
+
+    The exchanges' device work runs on a stream of this module's, never the null stream
+    (an operation there makes every later launch on the encoders' lane streams slower,
+    DESIGN §2); the call returns once that stream is idle."""
+    import torch
+
+    if out.device.type != "cuda":
+        return _encode_stripe_dist(enc, rgb_ptr, stride, width, height, quality, out, maxval, group, restart)
+    side = _SIDE.get(out.device.index)
+    if side is None:
+        side = _SIDE[out.device.index] = torch.cuda.Stream(device=out.device)
+    with torch.cuda.stream(side):
+        total = _encode_stripe_dist(enc, rgb_ptr, stride, width, height, quality, out, maxval, group, restart)
+    side.synchronize()
+    return total
+
+
+_SIDE = {}  # device index -> the exchanges' stream
+
+
+def _encode_stripe_dist(enc, rgb_ptr, stride, width, height, quality, out, maxval, group, restart):
     import torch
     import torch.distributed as dist
 
