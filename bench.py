@@ -519,18 +519,31 @@ def solo_timing(J, local, frames, outd, args, fset: int, restart: int = 0):
     return tm, win
 
 
+def record_bytes(counts) -> float:
+    """K2's symbol records of one frame (kernels.hpp): 2 bytes per Huffman-coded symbol,
+    and a 2-byte continuation for each symbol whose size (AC) or category (DC) is above 6;
+    counts = the frame's four histograms (Encoder.symbol_stats)."""
+    c = np.asarray(counts, np.int64).reshape(4, 256)
+    s = np.arange(256)
+    size = np.where((np.arange(4)[:, None] & 1) == 1, s & 15, s)
+    return 2.0 * float(c.sum() + c[size > 6].sum())
+
+
+REC_WHAT = "16-bit symbol records (2 B per symbol, +2 B per size > 6)"
+
+
 def alg_bytes(npx: float, cb: float, rec_bytes: float, avg_jpeg: float):
     """Per-kernel and entropy-stage algorithmic bytes per frame: K1 reads
-    RGB8 and writes int16 coefficients; K2 reads the coefficients and writes one 4-byte
-    record per Huffman-coded symbol; the code kernel reads the records and writes the bit
+    RGB8 and writes int16 coefficients; K2 reads the coefficients and writes its 16-bit
+    symbol records (record_bytes); the code kernel reads the records and writes the bit
     stream (~ the .jpg size); the pack kernel reads it and writes the stuffed bytes."""
     alg = {
         "fdct_kernel": ((3.0 + cb) * npx, f"RGB8 read 3 B/px + int16 coefficients written {cb:g} B/px"),
-        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + symbol records written 4 B each"),
-        "entropy_code_kernel": (rec_bytes + avg_jpeg, "symbol records read 4 B each + bit stream written (~.jpg size)"),
+        "stats_kernel": (cb * npx + rec_bytes, f"coefficients read {cb:g} B/px + {REC_WHAT} written"),
+        "entropy_code_kernel": (rec_bytes + avg_jpeg, f"{REC_WHAT} read + bit stream written (~.jpg size)"),
         "entropy_pack_kernel": (2.0 * avg_jpeg, "bit stream read + stuffed .jpg bytes written"),
     }
-    stage = {"entropy_stage": (rec_bytes + avg_jpeg, "symbol records read 4 B each + .jpg bytes written")}
+    stage = {"entropy_stage": (rec_bytes + avg_jpeg, f"{REC_WHAT} read + .jpg bytes written")}
     return alg, stage
 
 
@@ -630,7 +643,8 @@ def run_dist_check(args, rank, local, world, pg):
     if os.environ.get("JPGE_BENCH_FAIL_RANK") == str(rank):
         raise SystemExit(3)
     if os.environ.get("JPGE_BENCH_HANG_RANK") == str(rank):  # (the phase watchdog's test)
-        PHASE("dist-check: stuck (test hook)")
+        # (its own limit: under a loaded test host the other phases keep --phase-timeout's slack)
+        PHASE("dist-check: stuck (test hook)", float(os.environ.get("JPGE_BENCH_HANG_LIMIT", "0")) or None)
         time.sleep(3600)
     barrier(pg)
     dt = max_over_ranks(pg, 0.001 * (rank + 1))
@@ -733,10 +747,10 @@ def run_striped16k(args, rank, local, world, pg):
                                         restart=restart)
         sym_enc = J.Encoder(local, lanes=1)
         hrows = rgb if world == 1 else src.view(hs, W, 3).cpu().numpy()
-        syms = int(sym_enc.symbol_stats(hrows, quality=args.quality)[0].sum())
+        rb = record_bytes(sym_enc.symbol_stats(hrows, quality=args.quality)[0])
         sym_enc.close()
         del hrows
-        alg, stage_alg = alg_bytes(W * hs, 3.0, 4.0 * syms, float(n) * hs / H)
+        alg, stage_alg = alg_bytes(W * hs, 3.0, rb, float(n) * hs / H)
         stages_solo = kernel_rooflines(tm_solo, alg, stage_alg, {}, W * hs)
         roofline = solo_headline(stages_solo, alg, 1, ms_step)
     else:
@@ -970,9 +984,9 @@ def run_batch1080(args, rank, local, world, pg):
         fset = max(1, min(4, (4 * 3840 * 2160) // (W * H)))
         tm_solo, solo_win = solo_timing(J, local, sfr, sout, args, fset)
         tm_solo1, solo1_win = solo_timing(J, local, sfr, sout, args, 1)
-        syms = [int(enc.symbol_stats(host[i], quality=args.quality)[0].sum()) for i in share[:len(sfr)]]
+        rbs = [record_bytes(enc.symbol_stats(host[i], quality=args.quality)[0]) for i in share[:len(sfr)]]
         avg_jpeg_rank = sum(lens) / max(1, len(lens))
-        alg, stage_alg = alg_bytes(W * H, 3.0, 4.0 * sum(syms) / len(syms), avg_jpeg_rank)
+        alg, stage_alg = alg_bytes(W * H, 3.0, sum(rbs) / len(rbs), avg_jpeg_rank)
         traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H)
         stages_solo = kernel_rooflines(tm_solo, alg, stage_alg, traffic, W * H)
         stages_solo1 = kernel_rooflines(tm_solo1, alg, stage_alg, traffic, W * H)
@@ -1180,11 +1194,11 @@ def run_frames(args, rank, local, world, pg):
     traffic = load_pmc_traffic(os.path.join(ROOT, "profiles"), W, H) if args.subsampling == 420 else {}
     yh, yv = J.SUBSAMPLING[args.subsampling]
     cb = 2.0 * 64 * (yh * yv + 2) / (64 * yh * yv)  # int16 coefficient bytes per pixel (4:2:0: 3)
-    # symbol records (4 B each, one per Huffman-coded symbol): written by K2, read by K3;
-    # the count per frame from every distinct input's histograms (whether or not a pass
-    # sampled it), averaged over the step's frames (frame i = input i mod D)
-    syms = [int(enc.symbol_stats(host[d], quality=args.quality)[0].sum()) for d in range(D)] if rank == 0 else [0]
-    rec_bytes = 4.0 * sum(syms[i % len(syms)] for i in range(F)) / F
+    # symbol records (record_bytes): written by K2, read by K3; per frame from every
+    # distinct input's histograms (whether or not a pass sampled it), averaged over the
+    # step's frames (frame i = input i mod D)
+    rbs = [record_bytes(enc.symbol_stats(host[d], quality=args.quality)[0]) for d in range(D)] if rank == 0 else [0.0]
+    rec_bytes = sum(rbs[i % len(rbs)] for i in range(F)) / F
     alg, stage_alg = alg_bytes(npx, cb, rec_bytes, avg_jpeg)
 
     stages = kernel_rooflines(tm, alg, stage_alg, traffic, npx)  # in situ (lanes overlap: diagnostic)

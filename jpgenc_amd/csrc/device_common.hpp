@@ -57,6 +57,8 @@ namespace dev {
 // buffer-descriptor loads return 4 x u32 as a vector type
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 as_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 as_u2(u32x2 v) { return make_uint2(v.x, v.y); }
 
 // natural (row-major) index -> zig-zag position (inverse of Coding.hpp:57-81)
 static __constant__ uint8_t kNatToZz[64] = {

@@ -301,7 +301,7 @@ struct Encoder::Slot {
     uint8_t* d_ctl = nullptr;
     uint8_t* d_ubuf = nullptr;  // unstuffed entropy-coded segment (K3 internal)
     size_t cap_ubuf = 0;
-    uint32_t* d_recs = nullptr;    // K2's symbol records, kTileRecords per entropy tile
+    uint16_t* d_recs = nullptr;    // K2's symbol records, kTileRecords per entropy tile
     uint32_t* d_tcount = nullptr;  // records per tile
     size_t cap_tiles = 0;          // (capacities: records, in words; tiles)
     size_t cap_recs = 0;

@@ -31,8 +31,11 @@ using namespace dev;
 
 constexpr int kK3Groups = 2;  // code kernel: 4-record groups per thread and round (one scan and barrier per round)
 // waves per SIMD: one group fits 64 VGPRs at 8 (+4% in the pipeline over 4); two groups
-// need 72 (7 waves): +0.7% over one group at 8 (2 pairs on one box; 6 waves: +0.3%)
-constexpr int kK3Wpe = kK3Groups > 1 ? 7 : 8;
+// need 66-72 (7 waves, 3 workgroups per CU): +0.7% over one group at 8.  With 16-bit
+// records, 0xFF counters packed two per register fit two groups in 64 VGPRs (8 waves, 4
+// workgroups per CU): the kernel alone 4 us faster per set, the pipeline 1.3% slower at
+// Q90 (+1.6% at Q100); 3 workgroups per CU leave the other lanes' kernels more room.
+constexpr int kK3Wpe = 7;
 constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
 constexpr int kK3Waves = kK3Threads / 64;
@@ -60,7 +63,7 @@ struct K3Lds {
     // the tile's big-endian bit stream (offset 0 of the kernel's only __shared__ object,
     // so 16-byte aligned; an alignas(16) here made the compiler spill 8 VGPRs)
     uint32_t stage[kStageWords];
-    uint32_t tab[4 * 256];        // lds_tab_entry: code | (len + extra bits) << 16 | extra bits << 24
+    uint2 tab[4 * 256];           // lds_tab_entry, indexed by a record's bits 6-15
     uint32_t tcnt[kTcntSlots];    // symbol records of each sub-stream of the workgroup's tiles
     uint32_t tcum[kTcntSlots + 2];  // their first padded stream indices, the total, then a sentinel
     alignas(8) uint32_t wsum[2][kK3Waves];  // the rounds' scans, alternating (no barrier between rounds); the placement's 64-bit scans
@@ -80,26 +83,26 @@ __device__ __forceinline__ uint32_t byte_range(int lo, int hi) {
     return ge & lt & 0x80808080u;
 }
 
-// The code kernel's LDS table entry for table t, symbol s: the code (bits 0-15), the
-// code length plus the symbol's extra-bit count (bits 16-23), the extra-bit count
-// (bits 24-31: AC, the symbol's size; DC, its category).  Host entries are
-// (len << 16) | code.
-// (A code length is at most 16 and a DC category at most 15: clamped, so whatever the
-// tables hold, a string stays within the 27 bits the stage and region bounds assume.)
-__device__ __forceinline__ uint32_t lds_tab_entry(uint32_t host, uint32_t i) {
-    const uint32_t t = i >> 8, sym = i & 0xFF;
-    const uint32_t nb = (t & 1) ? (sym & 15) : min(sym & 31, 11u);
+// The code kernel's LDS table entry for record index i = record >> 6 (kernels.hpp):
+// table t = i >> 8, symbol s = i & 255.  .x = the code shifted past the extra bits the
+// record holds, .y = that count | (code length + count) << 8.  A continuation (an AC
+// index of size 0 and run n in 1..14) is n raw bits.  Host entries are (len << 16) | code.
+// (Code lengths and bit counts clamped: whatever the tables and records hold, a record
+// codes at most 16 + 6 bits, the bound the stage and region sizes assume.)
+__device__ __forceinline__ uint2 lds_tab_entry(const uint32_t* tables, uint32_t i) {
+    const uint32_t s = i & 0xFF, size = (i & 0x100) ? s & 15 : s, run = s >> 4;
+    const bool cont = (i & 0x100) && size == 0 && run - 1u < 14u;
+    const uint32_t host = cont ? 0u : tables[i], nb = min(cont ? run : size, kRecXBits);
     const uint32_t len = min(host >> 16, 16u);
-    return (nb << 24) | ((len + nb) << 16) | (host & 0xFFFF & ((1u << len) - 1u));
+    return make_uint2((host & 0xFFFF & ((1u << len) - 1u)) << nb, nb | ((len + nb) << 8));
 }
-// One symbol record (K2, kernels.hpp: table << 24 | symbol << 16 | extra bits) as code
-// bits: the table's code, then the extra bits; returns the bit count (<= 16 + 16).
-// (The record's top half is the entry's index; the extra-bit count rides in the entry,
-// so a record costs a read, two extracts, a shift and an OR.)
-__device__ __forceinline__ uint32_t rec_bits(uint32_t r, const uint32_t* tab, uint32_t& bits) {
-    const uint32_t ent = tab[r >> 16];
-    bits = ((ent & 0xFFFF) << (ent >> 24)) | (r & 0xFFFF);
-    return (ent >> 16) & 0xFF;
+// The record in bits [off, off + 16) of w as code bits: the table's code, then the extra
+// bits the record holds; returns the bit count (<= 16 + 6).  (A read, two bit-field
+// extracts, an OR and a shift; v_bfe takes the width from the entry's low 5 bits.)
+__device__ __forceinline__ uint32_t rec_bits(uint32_t w, uint32_t off, const uint2* tab, uint32_t& bits) {
+    const uint2 e = tab[__builtin_amdgcn_ubfe(w, off + 6u, 10u)];
+    bits = e.x | __builtin_amdgcn_ubfe(w, off, e.y);
+    return e.y >> 8;
 }
 
 // every workgroup's WgPlace from the records (the placement scan), kK3Threads threads
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
         export_hist<kK3Threads>(a.exp_hist, a.exp_cnt, a.exp_key, a.exp_seq, a.exp_seqv, tid);
     if (tid == 0) L.carry = 0;
     if (tid < 8) L.cnt8[tid] = 0;
-    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = lds_tab_entry(a.tables[i], (uint32_t)i);
+    for (int i = tid; i < 1024; i += kK3Threads) L.tab[i] = lds_tab_entry(a.tables, (uint32_t)i);
     // (the stage zeroed in 16-byte stores; with K2's: 185.8 vs 184.4 GPix/s over 3 pairs)
     static_assert(kStageWords % 4 == 0, "the stage zeroes in 16-byte stores");
     for (int i = tid; i < kStageWords / 4; i += kK3Threads) reinterpret_cast<uint4*>(L.stage)[i] = make_uint4(0, 0, 0, 0);
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
     const uint32_t gt0 = wt.seg * a.seg.tps + wt.t0;  // global number of the first tile
     constexpr uint32_t slot = kSubRecords;  // records per sub-stream
     const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * slot * 4, 0x00020000);
+        const_cast<uint16_t*>(a.recs + (uint64_t)gt0 * kTileRecords), 0, ntl * slot * 2, 0x00020000);
     constexpr int kGroups = kK3Groups;            // groups of 4 records per thread and round
     constexpr uint32_t kRound = 4 * kGroups * kK3Threads;  // records per round
     // The workgroup's records are one stream over its tiles: tile t's count padded to a
@@ -177,21 +180,21 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
     uint32_t cs = 0;  // this thread's sub-stream cursor
     // the thread's 4 records from stream index i (nvalid: how many are records); the
     // cursor walks the padded prefix (the sentinel past the total stops it at ntl)
-    auto rec_load = [&](uint32_t i, uint32_t& nvalid) -> uint4 {
+    auto rec_load = [&](uint32_t i, uint32_t& nvalid) -> uint2 {
         while (i >= L.tcum[cs + 1]) ++cs;
         uint32_t off = 0xFFFFFFF0u;  // (past the end: out of range, zeros)
         nvalid = 0;
         if (cs < (uint32_t)ntl) {
             const uint32_t rel = i - L.tcum[cs], c = L.tcnt[cs];
             nvalid = c > rel ? min(c - rel, 4u) : 0u;
-            off = (cs * slot + rel) * 4;
+            off = (cs * slot + rel) * 2;
         }
-        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rec_rs, off, 0, 0));
+        return as_u2(__builtin_amdgcn_raw_buffer_load_b64(rec_rs, off, 0, 0));
     };
     constexpr uint32_t kStageBits = (kStageWords - 2) * 32;
-    constexpr uint32_t kRoundMaxBits = kRound * 27;  // (a record codes at most 16 + 11 bits)
+    constexpr uint32_t kRoundMaxBits = kRound * 22;  // (a record codes at most 16 + 6 bits)
     static_assert(kStageBits > kRoundMaxBits, "the stage holds a round");
-    uint4 nxt[kGroups];
+    uint2 nxt[kGroups];
     uint32_t nvn[kGroups];
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) nxt[g] = rec_load(4 * (kGroups * tid + g), nvn[g]);
@@ -202,14 +205,14 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
 
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
-            const uint4 rv = nxt[g];
+            const uint2 rv = nxt[g];
             const uint32_t nv = nvn[g];
             nxt[g] = rec_load(r0 + kRound + 4 * (kGroups * tid + g), nvn[g]);  // the next round's (prefetch)
-            const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+            const uint32_t rr[4] = {rv.x, rv.x, rv.y, rv.y};
             gl[g] = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t n = rec_bits(rr[q], L.tab, cb[g][q]);
+                const uint32_t n = rec_bits(rr[q], (uint32_t)(q & 1) * 16u, L.tab, cb[g][q]);
                 cl[g][q] = (uint32_t)q < nv ? n : 0u;
                 gl[g] += cl[g][q];
             }

@@ -138,15 +138,21 @@ JPGE_HD inline WgTiles wg_tiles(const SegLayout& L, uint32_t w) {
 }
 
 // Symbol records (K2 -> K3): the entropy-coded symbols of a tile in stream order,
-// one u32 each: table << 24 | symbol << 16 | extra bits (table 0 Y-DC, 1 Y-AC,
-// 2 C-DC, 3 C-AC; the extra bits' count is the symbol's category: symbol & 15 for
-// AC, the symbol itself for DC).  A block codes at most 64 symbols (DC + 63 AC, or
-// DC + 62 AC + EOB; a zero run long enough for a ZRL removes a coefficient), so a
-// tile's records fit kTileRecords words; tile t's sit at recs + t * kTileRecords,
-// its count at tcount[t].  Tiles are the entropy partition's (seg_layout), numbered
-// segment by segment.
-constexpr int kRecPerBlock = 64;
+// 16 bits each (round 6; 32-bit records had been 38% of a 4K frame's HBM bytes):
+//   table << 14 | run << 10 | size << 6 | x     (table 0 Y-DC, 1 Y-AC, 2 C-DC, 3 C-AC;
+//   a DC symbol is its category with run 0; EOB run 0 size 0; ZRL run 15 size 0), x = the
+//   top min(size, 6) of the symbol's extra bits;
+//   continuation: the component's AC table << 14 | n << 10 | the n (1..5) low extra bits
+//   the record before it could not hold (size >= 7); run n with size 0 is no JPEG symbol
+//   (Coding.hpp:148-196 codes zero runs only as ZRL and EOB), so it never collides with one.
+// The code kernel indexes one 64-bit LDS entry per record by record >> 6.  A block codes
+// at most 64 symbols (DC + 63 AC, or DC + 62 AC + EOB; a zero run long enough for a ZRL
+// removes a coefficient), each with at most one continuation, so a tile's records fit
+// kTileRecords halfwords; tile t's sit at recs + t * kTileRecords.  Tiles are the entropy
+// partition's (seg_layout), numbered segment by segment.
+constexpr int kRecPerBlock = 128;
 constexpr int kTileRecords = kEntropyTile * kRecPerBlock;
+constexpr uint32_t kRecXBits = 6;  // extra bits a head record holds
 // A tile's records are written as kRecSub sub-streams, one per wave of the
 // statistics kernel: sub-stream j of a tile of nb blocks holds blocks
 // [j*nb/kRecSub, (j+1)*nb/kRecSub) of the tile, at recs + t*kTileRecords +
@@ -167,7 +173,7 @@ struct StatsArgs {
     // Cb block, and the image's Cb block count (every Cr key follows all Cb keys)
     uint64_t key_y0 = 0, key_c0 = 0, key_ncb = 0;
     SegLayout seg;       // the entropy partition: the tiles the records are written in
-    uint32_t* recs;      // [tiles][kTileRecords] symbol records
+    uint16_t* recs;      // [tiles][kTileRecords] symbol records
     uint32_t* tcount;    // [tiles][kRecSub] records per sub-stream
     uint32_t wgs = 0;    // workgroup count (0 = 3 per CU; the pipeline passes its own, stats_grid)
     uint64_t* dbg;
@@ -209,7 +215,7 @@ constexpr uint32_t kExtPlace = 4u;     // pack kernel reads WgPlace (entropy_sca
 
 struct EntropyArgs {
     const int16_t* coef;
-    const uint32_t* recs;    // the statistics kernel's symbol records (kTileRecords per tile)
+    const uint16_t* recs;    // the statistics kernel's symbol records (kTileRecords per tile)
     const uint32_t* tcount;  // records per tile
     Geometry g;
     const uint32_t* tables;  // [4][256] (len << 16) | code, followed by the header bytes

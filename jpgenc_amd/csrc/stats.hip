@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     uint32_t* const cnt = L.cnt + (uint32_t)(lane & (kWCopies - 1)) * kWCopyWords;
     const uint32_t shl = (uint32_t)(64 - lane) & 63u;
     const uint64_t lanes_ac = ~1ull;  // every lane but the DC
-    const uint32_t dc_tab = lane == 0 ? 1u << 24 : 0u;  // (a record's table byte: 2t + 1 -> 2t)
+    const uint32_t dc_tab = lane == 0 ? 1u << 14 : 0u;  // (a record's table bits: 2t + 1 -> 2t)
     const uint32_t dc_run = lane == 0 ? 16u : 0u;  // (lane 0's run: its counter word is the DC table's, kDcOff)
     int16_t* st16 = reinterpret_cast<int16_t*>(L.stage[wv]);
     uint4* st4 = reinterpret_cast<uint4*>(L.stage[wv]);
@@ -213,15 +213,16 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         JPGE_ACC(1, tq);
 
         // ---- the blocks ----
-        uint32_t* srec = a.recs + (uint64_t)(s / kRecSub) * kTileRecords + (s % kRecSub) * kSubRecords;
-        const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(srec, 0, kSubRecords * 4, 0x00020000);
+        uint16_t* srec = a.recs + (uint64_t)(s / kRecSub) * kTileRecords + (s % kRecSub) * kSubRecords;
+        const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(srec, 0, kSubRecords * 2, 0x00020000);
         uint32_t base = 0;   // the block's first record (its DC) in the sub-stream
         // one block's fields (lane p: zig-zag position p)
         struct Blk {
             uint64_t M, em;     // AC non-zeros; the lanes with a record (lane 0: the DC; lane 63: non-zero, or the EOB)
-            uint32_t rk, run;   // record index in the block (DC = 0), zeros before the coefficient
+            uint32_t rk, run;   // record index in the block (DC = 0; continuations before it counted), zeros before the coefficient
+            uint64_t bg;        // the lanes whose extra bits need a continuation record (size >= 7; rare)
             uint32_t rec, w;    // the record; its counter / key word
-            uint32_t Tj, acbj, acw;  // the block's AC table (top byte), key base, table base word
+            uint32_t Tj, acbj, acw;  // the block's AC table (record bits 14-15), key base, table base word
             bool zrl;           // a run of 16+ zeros before a non-zero
         };
         // kExact: runs exact (every length; the ZRL path).  Otherwise exact up to 31:
@@ -236,31 +237,54 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             b.M = B1 & lanes_ac;
             b.acbj = __builtin_amdgcn_readlane(acb, jb);    // (+ 2p: the key; the EOB lane 63: text * 128 + 126 + d)
             const uint32_t d = b.acbj & 1u;                  // (scalar: 1 for the chroma tables)
-            b.Tj = 0x01000000u + (d << 25);                  // the AC table, as a record's top byte
+            b.Tj = (1u << 14) + (d << 15);                   // the AC table, as a record's top bits
             b.acw = d * tab_base(3);                         // its first counter / key word (tab_base(1) = 0)
             b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0u));
             if constexpr (kExact) b.run = (uint32_t)__builtin_clzll(B1 << shl);  // (lane 0: unused)
             else b.run = (uint32_t)__builtin_clz((uint32_t)((B1 << shl) >> 32) | 1u);
-            const int cat = __builtin_amdgcn_frexp_expf((float)c);
-            const uint32_t bits = extra_bits(c, cat);
+            const uint32_t cat = (uint32_t)__builtin_amdgcn_frexp_expf((float)c);
+            const uint32_t bits = extra_bits(c, (int)cat);
             // (the EOB lane: 0; the DC lane: 16)
             const uint32_t rr = __builtin_amdgcn_inverse_ballot_w64(b.M) ? (kExact ? b.run & 15u : b.run) : dc_run;
             // lane 0 (the DC position, where the stage holds the block's DC difference)
             // codes the block's DC symbol like an AC lane: its record (its table: the AC
-            // table's number less one; the run of 16 sets a bit the table byte has) at the
-            // block's first record (rank 0), its count in the DC table's word (kDcOff past
-            // the AC table's first), its key as text index * 128 + d (the flush divides
-            // it back).  Stored after the sub-stream, the DC records had rewritten lines
-            // already written back (K2 wrote 1.24x its record bytes); counted after the
-            // sub-stream, they cost a pass of their own.
-            b.rec = (b.Tj | (((rr << 4) | (uint32_t)cat) << 16) | bits) ^ dc_tab;
+            // table's number less one; the run of 16 sets a bit the table bits have; its
+            // category where an AC record has its run) at the block's first record (rank
+            // 0), its count in the DC table's word (kDcOff past the AC table's first), its
+            // key as text index * 128 + d (the flush divides it back).  Stored after the
+            // sub-stream, the DC records had rewritten lines already written back (K2 wrote
+            // 1.24x its record bytes); counted after the sub-stream, they cost a pass of
+            // their own.
+            // a size above 6 keeps its extra bits' top 6 in the record and the rest in a
+            // continuation right after it (kernels.hpp; the fast path fixes such blocks up
+            // in cont(), from the record's low 6 bits)
+            b.bg = __builtin_amdgcn_ballot_w64(cat > kRecXBits);
+            uint32_t x = bits & 63u;
+            if constexpr (kExact) {
+                x = bits >> __builtin_elementwise_sub_sat(cat, kRecXBits);
+                b.rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(b.bg >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b.bg, b.rk));
+            }
+            b.rec = ((b.Tj | (rr << 10) | (cat << 6)) ^ dc_tab) | x;
             b.w = b.acw + (uint32_t)cat + kRunStride * rr;
             b.em = B1 | (1ull << 63);
             b.zrl = (__ballot(b.run >= 16u) & b.M) != 0;
             return b;
         };
-        // (general form, every block with ZRLs) block jb's records from `base`, histogram
-        // and keys, all from its staged coefficient c; returns its record count
+        // (fast path, a block with size >= 7 symbols: uniform, rare at Q90) each such record
+        // keeps its extra bits' top 6, and its continuation right after it the rest: the
+        // records after it move one further, the block's count grows by one
+        auto cont = [&](uint64_t bg, int c, uint32_t Tj, uint32_t b0, uint32_t& rk, uint32_t& rec, uint32_t& n) {
+            if (!bg) return;
+            const uint32_t cat = (uint32_t)__builtin_amdgcn_frexp_expf((float)c);
+            const uint32_t sh = __builtin_elementwise_sub_sat(cat, kRecXBits), bits = extra_bits(c, (int)cat);
+            rec = (rec & ~63u) | (bits >> sh);
+            rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bg >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bg, rk));
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(Tj | (sh << 10) | (bits & ((1u << sh) - 1u))), rrs,
+                                                  __builtin_amdgcn_inverse_ballot_w64(bg) ? (b0 + rk + 1u) * 2u : 0x80000000u, 0, 0);
+            n += (uint32_t)__builtin_popcountll(bg);
+        };
+        // (general form, every block with ZRLs) block jb's records from
+        // `base`, histogram and keys, all from its staged coefficient c; returns its record count
         auto emit = [&](int c, uint32_t jb, uint32_t base) -> uint32_t {
             Blk b = prep(c, jb, std::true_type{});
             uint32_t zt = 0;
@@ -270,7 +294,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 zt = __builtin_amdgcn_readlane(zi, 63);
                 b.rk += zi;
                 if (nzr) {
-                    const uint32_t zrec = b.Tj | (0xF0u << 16);
+                    const uint16_t zrec = (uint16_t)(b.Tj | (15u << 10));
                     for (uint32_t z = 1; z <= nzr; ++z) srec[base + b.rk - z] = zrec;
                     const uint32_t wz = b.acw + kRunStride * 15u;  // (symbol 0xF0)
                     atomicAdd(&cnt[wz], nzr);
@@ -279,12 +303,16 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 }
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b.em)) {
-                srec[base + b.rk] = b.rec;
+                srec[base + b.rk] = (uint16_t)b.rec;
+                if (__builtin_amdgcn_inverse_ballot_w64(b.bg)) {  // (its extra bits past the record's 6)
+                    const uint32_t cat = (uint32_t)__builtin_amdgcn_frexp_expf((float)c), sh = cat - kRecXBits;
+                    srec[base + b.rk + 1] = (uint16_t)(b.Tj | (sh << 10) | (extra_bits(c, (int)cat) & ((1u << sh) - 1u)));
+                }
                 atomicAdd(&cnt[b.w], 1u);
                 const uint32_t kk = b.acbj + k2p;
                 if (kk < L.key[b.w]) atomicMin(&L.key[b.w], kk);
             }
-            return (uint32_t)__builtin_popcountll(b.em) + zt;  // DC, the non-zeros and the EOB, the ZRLs
+            return (uint32_t)__builtin_popcountll(b.em) + zt + (uint32_t)__builtin_popcountll(b.bg);  // DC, non-zeros, EOB, ZRLs, continuations
         };
 #pragma unroll
         for (int ch = 0; ch < kWRows; ++ch) {  // 8-block chunks: stage one, load the next sub-stream's into its registers
@@ -307,12 +335,18 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                 const Blk A = prep(cA, jb, std::false_type{}), B = prep(cB, jb + 1, std::false_type{});
                 uint32_t baseB;
                 if (!(A.zrl || B.zrl)) {
+                    uint32_t recA = A.rec, recB = B.rec, rkA = A.rk, rkB = B.rk;
+                    uint32_t nA = (uint32_t)__builtin_popcountll(A.em), nB = (uint32_t)__builtin_popcountll(B.em);
+                    if (A.bg | B.bg) {
+                        cont(A.bg, cp[0], A.Tj, base, rkA, recA, nA);
+                        cont(B.bg, cp[64], B.Tj, base + nA, rkB, recB, nB);
+                    }
                     // lanes without a record store out of range (dropped); their counter adds
                     // are masked off
-                    baseB = base + (uint32_t)__builtin_popcountll(A.em);
+                    baseB = base + nA;
                     const bool ia = __builtin_amdgcn_inverse_ballot_w64(A.em), ib = __builtin_amdgcn_inverse_ballot_w64(B.em);
-                    __builtin_amdgcn_raw_buffer_store_b32(A.rec, rrs, ia ? (base + A.rk) * 4u : 0x80000000u, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(B.rec, rrs, ib ? (baseB + B.rk) * 4u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)recA, rrs, ia ? (base + rkA) * 2u : 0x80000000u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)recB, rrs, ib ? (baseB + rkB) * 2u : 0x80000000u, 0, 0);
                     if (ia) atomicAdd(&cnt[A.w], 1u);
                     if (ib) atomicAdd(&cnt[B.w], 1u);
                     // (every lane reads its word: a lane without a record has c = 0, so its
@@ -327,7 +361,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
                         if (__builtin_amdgcn_inverse_ballot_w64(fA)) atomicMin(&L.key[A.w], kkA);
                         if (__builtin_amdgcn_inverse_ballot_w64(fB)) atomicMin(&L.key[B.w], kkB);
                     }
-                    base = baseB + (uint32_t)__builtin_popcountll(B.em);
+                    base = baseB + nB;
                 } else {  // (a ZRL block: both again from the stage, exactly)
                     baseB = base + emit(cp[0], jb, base);
                     base = baseB + emit(cp[64], jb + 1, baseB);

@@ -129,9 +129,10 @@ def test_bench_phase_watchdog_names_a_stuck_rank():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["JPGE_BENCH_HANG_RANK"] = "1"  # rank 1 sleeps inside a named phase; rank 0 waits in a barrier
     env["JPGE_BENCH_DEVICE_COUNT"] = "2"
+    env["JPGE_BENCH_HANG_LIMIT"] = "4"  # the stuck phase's own limit; start-up keeps --phase-timeout
     t = time.monotonic()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "dist-check",
-                        "--phase-timeout", "4", "--pg-timeout", "60"], env=env, capture_output=True, text=True,
+                        "--phase-timeout", "40", "--pg-timeout", "60"], env=env, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 124, r.stderr[-2000:]
     assert "rank 1: phase 'dist-check: stuck (test hook)' exceeded its 4 s limit" in r.stderr
