@@ -30,11 +30,11 @@ namespace {
 using namespace dev;
 
 constexpr int kK3Groups = 2;  // code kernel: 4-record groups per thread and round (one scan and barrier per round)
-// waves per SIMD: one group fits 64 VGPRs at 8 (+4% in the pipeline over 4); two groups
-// need 66-72 (7 waves, 3 workgroups per CU): +0.7% over one group at 8.  With 16-bit
-// records, 0xFF counters packed two per register fit two groups in 64 VGPRs (8 waves, 4
-// workgroups per CU): the kernel alone 4 us faster per set, the pipeline 1.3% slower at
-// Q90 (+1.6% at Q100); 3 workgroups per CU leave the other lanes' kernels more room.
+// waves per SIMD: the target is 7, and with 16-bit records and each group's bits
+// concatenated before the round's scan the kernel takes 60 VGPRs, so it runs at 8 (4
+// workgroups per CU): the pipeline +1.0% at Q90 and +2.8% at Q100 over the 66-VGPR form
+// (3 per CU), and over an LDS-padded form held at 3 per CU (-3.6%); three groups per
+// round (72 VGPRs) -3.4%.
 constexpr int kK3Wpe = 7;
 constexpr int kK3Blocks = kEntropyTile;
 constexpr int kK3Threads = kK3Blocks * kPartsPerBlock;  // 512
@@ -201,20 +201,27 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
     uint32_t lead = 0, pos = 0;  // bit position in the stage (lead: the carried partial word's bits)
     uint32_t par = 0;            // scan buffer of this round
     for (uint32_t r0 = 0; r0 < total; r0 += kRound) {
-        uint32_t cb[kGroups][4], cl[kGroups][4], gl[kGroups], tl = 0;
+        // per group: its records' bits concatenated (acc: exact when they total <= 64 bits)
+        // and their count; the records themselves for the rare longer group
+        uint64_t acc[kGroups];
+        uint32_t gl[kGroups], tl = 0;
+        uint2 rvs[kGroups];
+        uint32_t nvs[kGroups];
 
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
-            const uint2 rv = nxt[g];
-            const uint32_t nv = nvn[g];
+            rvs[g] = nxt[g];
+            nvs[g] = nvn[g];
             nxt[g] = rec_load(r0 + kRound + 4 * (kGroups * tid + g), nvn[g]);  // the next round's (prefetch)
-            const uint32_t rr[4] = {rv.x, rv.x, rv.y, rv.y};
+            const uint32_t rr[4] = {rvs[g].x, rvs[g].x, rvs[g].y, rvs[g].y};
             gl[g] = 0;
+            acc[g] = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t n = rec_bits(rr[q], (uint32_t)(q & 1) * 16u, L.tab, cb[g][q]);
-                cl[g][q] = (uint32_t)q < nv ? n : 0u;
-                gl[g] += cl[g][q];
+                uint32_t cb;
+                const uint32_t n = (uint32_t)q < nvs[g] ? rec_bits(rr[q], (uint32_t)(q & 1) * 16u, L.tab, cb) : 0u;
+                acc[g] = (acc[g] << n) | (n ? (uint64_t)cb : 0ull);
+                gl[g] += n;
             }
             tl += gl[g];
         }
@@ -235,10 +242,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
         // record.  More than 64 bits (rare: four long codes) take the per-record path.
         const uint32_t tg = gl[g];
         if (tg && tg <= 64) {
-            uint64_t acc = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc = (acc << cl[g][q]) | (cl[g][q] ? (uint64_t)cb[g][q] : 0ull);
-            const uint64_t A = acc << (64 - tg);  // MSB-aligned
+            const uint64_t A = acc[g] << (64 - tg);  // MSB-aligned
             const uint32_t sh = bp & 31, w = bp >> 5, end = sh + tg;
             const uint32_t hi = (uint32_t)(A >> 32), lo = (uint32_t)A;
             atomicOr(&L.stage[w], hi >> sh);
@@ -249,14 +253,17 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
                 if (end > 64) atomicOr(&L.stage[w + 2], lo << (32 - sh));
             }
             bp += tg;
-        } else {
+        } else if (tg) {
+            const uint32_t rr[4] = {rvs[g].x, rvs[g].x, rvs[g].y, rvs[g].y};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             // each record into the one or two stage words it spans (a branch per record:
             // a branch-free 64-bit form ran 6 us slower per 4K frame)
-            if (cl[g][q]) {
-                const uint32_t sh = bp & 31, n = cl[g][q];
-                const uint32_t v = cb[g][q] << (32 - n);  // MSB-aligned (n >= 1)
+            uint32_t cb;
+            const uint32_t n = (uint32_t)q < nvs[g] ? rec_bits(rr[q], (uint32_t)(q & 1) * 16u, L.tab, cb) : 0u;
+            if (n) {
+                const uint32_t sh = bp & 31;
+                const uint32_t v = cb << (32 - n);  // MSB-aligned (n >= 1)
                 atomicOr(&L.stage[bp >> 5], v >> sh);
                 if (sh + n > 32) atomicOr(&L.stage[(bp >> 5) + 1], v << (32 - sh));
                 bp += n;
