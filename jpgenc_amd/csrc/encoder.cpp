@@ -448,7 +448,6 @@ int Encoder::open(int device, std::unique_ptr<Encoder>& out, int lanes) {
     std::unique_ptr<Encoder> e(new Encoder());
     e->device_ = device;
     if (const char* ew = std::getenv("JPGE_ENTROPY_WGS")) e->entropy_wgs_ = (uint32_t)std::strtoul(ew, nullptr, 10);
-    if (const char* dg = std::getenv("JPGE_DIAG")) e->diag_ = (uint32_t)std::strtoul(dg, nullptr, 10);
     if (const char* sw = std::getenv("JPGE_STATS_WGS")) e->stats_wgs_ = (uint32_t)std::strtoul(sw, nullptr, 10);
     e->fdct_wgs_ = (uint32_t)env_int("JPGE_FDCT_WGS", 0, 0, 65536);
     e->stamps_file_ = std::getenv("JPGE_STAMPS_FILE");
@@ -739,7 +738,6 @@ EntropyArgs Encoder::entropy_args(Slot& s) {
     e.seq = s.seq;
     e.ubuf = s.d_ubuf;
     e.wgs = entropy_wgs_;
-    e.diag = diag_;
     e.seed = s.seed;
     e.rst = s.rst;
     e.seg = slot_layout(s);

@@ -193,7 +193,6 @@ class Encoder {
     SegLayout layout(const Geometry& g) const { return seg_layout(g, restart_mcus_, entropy_wgs()); }
     // the entropy partition a slot's current frame runs on
     SegLayout slot_layout(const Slot& s) const;
-    uint32_t diag_ = 0;         // JPGE_DIAG: diagnostic kernel switches (experiments only)
     uint32_t fdct_wgs_ = 0;     // JPGE_FDCT_WGS: pipeline transform grid (0: fdct_grid's cap)
     int lookahead_ = 2;         // JPGE_LOOKAHEAD: frames transformed ahead of an entropy launch
     int drain_lag_ = 1;         // JPGE_DRAIN_LAG: iterations between an entropy launch and its drain

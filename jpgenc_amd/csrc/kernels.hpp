@@ -240,7 +240,6 @@ struct EntropyArgs {
     uint64_t* exp_seq;
     uint64_t exp_seqv;
     uint32_t wgs;            // workgroup count override (0 = automatic; tests)
-    uint32_t diag;           // diagnostic switches (JPGE_DIAG; 0 in production)
     DcSeed seed;             // DC chain predecessors (stripes)
     // placement (stripes / large grids): stream starts at global bit p_ext with q_ext
     // stuffing bytes before it; head_split = its first byte when p_ext & 7 != 0
