@@ -181,9 +181,14 @@ class Encoder {
     uint32_t stats_wgs_ = 0;    // JPGE_STATS_WGS: statistics workgroup count (diagnostics; clamped)
     uint32_t restart_mcus_ = 0; // restart interval (jpge_set_restart_interval)
     int mode_ = 420;            // subsampling mode (jpge_set_subsampling)
-    // entropy workgroups: the override, else 512 for a single lane (its frames' latency:
-    // -5 us at 4K) and seg_layout's default (384) beside other lanes (+3% throughput)
-    uint32_t entropy_wgs() const { return entropy_wgs_ ? entropy_wgs_ : (lanes_.size() == 1 ? 512u : 0u); }
+    // entropy workgroups: the override, else 512 for a single lane's lone frames (their
+    // latency: -5 us at 4K) and seg_layout's default (384, or 2 tiles per workgroup under
+    // 768 tiles) beside other lanes (+3% throughput) and for a single lane's frame sets
+    // (JPGE_SET: four 1080p frames per launch 49 -> 36 us for the code + pack kernels
+    // alone, 4K equal)
+    uint32_t entropy_wgs() const {
+        return entropy_wgs_ ? entropy_wgs_ : (lanes_.size() == 1 && set_ <= 1 ? 512u : 0u);
+    }
     // statistics workgroups: 2 per CU alone (4K: 29.1 us vs 30.8 at 3 per CU, 37-40 at
     // 1.5 or 1), 1 per CU beside other lanes (6 tiles per workgroup at 4K: its fixed
     // costs, the prologue, first load and flush, amortised; 256 vs 512: +1.6% in the

@@ -88,11 +88,6 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     __shared__ K2WLds L;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    static_assert((kWCopies * kWCopyWords) % 4 == 0 && kWKeyWords % 4 == 0, "16-byte initialisation");
-    for (int i = tid; i < (int)(kWCopies * kWCopyWords / 4); i += kWThreads)
-        reinterpret_cast<uint4*>(L.cnt)[i] = make_uint4(0, 0, 0, 0);
-    for (int i = tid; i < (int)(kWKeyWords / 4); i += kWThreads)
-        reinterpret_cast<uint4*>(L.key)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
 
     const uint32_t bpm = a.g.bpm, mw = a.g.mw, yh = a.g.yh, yv = a.g.yv();
     const uint32_t yhs = (uint32_t)__builtin_ctz(yh);
@@ -107,6 +102,33 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         s_hi = __builtin_amdgcn_readlane(v, 1);
     }
     const uint32_t ns = s_hi - s_lo;  // (<= kWMaxSubs: stats_grid)
+    // this wave's first sub-stream (s_lo + wv) is requested before the LDS initialisation
+    // and the workgroup's sub-stream table: its HBM latency overlaps them
+    const uint32_t lane_u = (uint32_t)lane;
+    uint4 cur[kWRows];
+    int dcs = 0;  // lane l < nb + 6: the DC of block b0 - 6 + l of the fetched sub-stream (0 before the frame)
+    auto load_row = [&](const __amdgpu_buffer_rsrc_t& rs, int i) {
+        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + 64 * i) * 16, 0, 0));
+    };
+    auto load_dcs_at = [&](uint32_t b0, uint32_t nb) {
+        const int32_t g = (int32_t)(b0 + lane_u) - 6;  // (block numbers < 2^25: launch_stats)
+        dcs = (lane_u < nb + 6 && g >= 0) ? a.coef[(uint64_t)(uint32_t)g * 64] : 0;
+    };
+    if ((uint32_t)wv < ns) {
+        uint64_t b;
+        uint32_t n;
+        sub_tile(a.seg, s_lo + (uint32_t)wv, b, n);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int16_t*>(a.coef + b * 64), 0, n * 128, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kWRows; ++i) cur[i] = load_row(rs, i);
+        load_dcs_at((uint32_t)b, n);
+    }
+    static_assert((kWCopies * kWCopyWords) % 4 == 0 && kWKeyWords % 4 == 0, "16-byte initialisation");
+    for (int i = tid; i < (int)(kWCopies * kWCopyWords / 4); i += kWThreads)
+        reinterpret_cast<uint4*>(L.cnt)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < (int)(kWKeyWords / 4); i += kWThreads)
+        reinterpret_cast<uint4*>(L.key)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint32_t i = tid; i <= ns; i += kWThreads) {  // their first blocks (block numbers < 2^32: launch_stats)
         uint64_t b;
         uint32_t n;
@@ -149,28 +171,13 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
     int16_t* st16 = reinterpret_cast<int16_t*>(L.stage[wv]);
     uint4* st4 = reinterpret_cast<uint4*>(L.stage[wv]);
 
-    uint4 cur[kWRows];
-    int dcs = 0;  // lane l < nb + 6: the DC of block b0 - 6 + l of the fetched sub-stream (0 before the frame)
     auto rows = [&](uint32_t si) {  // sub-stream si's coefficients through a buffer descriptor (zeros past its blocks)
         const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
         return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(a.coef + (uint64_t)b0 * 64), 0, nb * 128,
                                                  0x00020000);
     };
-    auto load_row = [&](const __amdgpu_buffer_rsrc_t& rs, int i) {
-        return as_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + 64 * i) * 16, 0, 0));
-    };
-    auto load_dcs = [&](uint32_t si) {
-        const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
-        const int32_t g = (int32_t)(b0 + (uint32_t)lane) - 6;  // (block numbers < 2^25: launch_stats)
-        dcs = ((uint32_t)lane < nb + 6 && g >= 0) ? a.coef[(uint64_t)(uint32_t)g * 64] : 0;
-    };
+    auto load_dcs = [&](uint32_t si) { load_dcs_at(L.sb0[si], L.sb0[si + 1] - L.sb0[si]); };
     uint32_t si = (uint32_t)wv;
-    if (si < ns) {
-        const __amdgpu_buffer_rsrc_t rs = rows(si);
-#pragma unroll
-        for (int i = 0; i < kWRows; ++i) cur[i] = load_row(rs, i);
-        load_dcs(si);
-    }
     while (si < ns) {
         const uint32_t b0 = L.sb0[si], nb = L.sb0[si + 1] - b0;
         const uint32_t s = s_lo + si;
@@ -383,8 +390,15 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
 
     const int rep = bid % kHistReplicas;
     const uint64_t ncb = a.key_ncb ? a.key_ncb : a.g.nmcu();  // Cb blocks of the whole image
-    for (int i = tid; i < 1024; i += kWThreads) {
-        const uint32_t t = (uint32_t)i >> 8, sy = (uint32_t)i & 255u;
+    // (a thread's two words; the global key's atomicMax unconditional: reading the key
+    // first to skip needless atomics held every workgroup one global round trip longer,
+    // K2 alone 68.6 -> 62.6 us per set of 4 4K frames without it)
+    static_assert(1024 == 2 * kWThreads, "two flush words per thread");
+    unsigned long long* gk = reinterpret_cast<unsigned long long*>(a.hist.key);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)j * kWThreads;
+        const uint32_t t = i >> 8, sy = i & 255u;
         if (!(t & 1) && sy >= 16) continue;  // (DC tables: categories < 16)
         const uint32_t w = tab_base(t) + (sy & 15u) + kRunStride * (sy >> 4);
         uint32_t c = 0;
@@ -398,9 +412,7 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
         else kb = a.key_c0 + cbase + ((k32 & 0x80000000u) ? ncb : 0ull);
         // (AC keys: text index * 128 + 2p + delta + d; DC keys were kept as text index * 128 + d)
         const uint64_t gkey = (t & 1) ? kb * 128ull + (k32 & 0x7FFFFFFFu) : kb + ((k32 & 0x7FFFFFFFu) >> 7);
-        const unsigned long long inv = ~gkey;
-        unsigned long long* gk = reinterpret_cast<unsigned long long*>(&a.hist.key[i]);
-        if (inv > *gk) atomicMax(gk, inv);
+        atomicMax(&gk[i], (unsigned long long)~gkey);
     }
     export_if_last();
     JPGE_STAMP(3);
