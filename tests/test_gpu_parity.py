@@ -309,3 +309,41 @@ def test_pipeline_shapes_bit_exact(wgs, w, h, kind, quality):
             assert enc.encode_batch(frames, quality=quality) == [_oracle.encode(f, quality) for f in frames]
     finally:
         enc.close()
+
+
+def _extreme_frame(w, h, seed):
+    # 8x8 blocks alternating black and white (DC differences of +-2040 at Q100: category
+    # 11, the largest; the DC continuation record) with single-pixel impulses and sharp
+    # edges inside some blocks (AC sizes up to 10: continuations of 1..4 bits)
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = (((y // 8) + (x // 8)) & 1).astype(np.uint8) * 255
+    rgb = np.repeat(base[:, :, None], 3, axis=2)
+    mask = rng.random((h, w)) < 0.02
+    rgb[mask] = 255 - rgb[mask]
+    edge = ((x % 8) < (y % 8)) & (((y // 8) * 3 + (x // 8)) % 5 == 0)
+    rgb[edge, 0] = 255 - rgb[edge, 0]
+    step = (((y // 8) * 7 + (x // 8)) % 11 == 0)  # blocks split into a black and a white half (AC size 10)
+    rgb[step] = np.where((x[step] % 8) < 4, 0, 255)[:, None]
+    return np.ascontiguousarray(rgb)
+
+
+@pytest.mark.parametrize("quality", [100, 97, 90, 50])
+@pytest.mark.parametrize("w,h", [(64, 48), (256, 136), (1000, 504)])
+def test_extreme_sizes_bit_exact(encoder, w, h, quality):
+    """The 16-bit symbol records' continuations (kernels.hpp): DC categories up to 11 and
+    AC sizes up to 10 (Coding.hpp:197-230), through the fast path's fix-up and the
+    general path, in single frames and a batch."""
+    rgb = _extreme_frame(w, h, w + h + quality)
+    want = _oracle.encode(rgb, quality)
+    assert encoder.encode(rgb, quality=quality) == want
+    assert encoder.encode_batch([rgb, rgb[::-1].copy()], quality=quality) == [want, _oracle.encode(rgb[::-1].copy(), quality)]
+
+
+def test_extreme_frame_reaches_the_largest_categories():
+    """(host) the frame above does reach DC category 11 and AC size 10 at Q100."""
+    rgb = _extreme_frame(256, 136, 1)
+    counts, _ = _oracle.stage_hist(rgb, 100)
+    counts = np.asarray(counts).reshape(4, 256)
+    assert counts[0, 11] > 0 or counts[2, 11] > 0
+    assert any(counts[1, (r << 4) | 10] or counts[3, (r << 4) | 10] for r in range(16))
