@@ -263,8 +263,9 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(kWWpe
             // 1.24x its record bytes); counted after the sub-stream, they cost a pass of
             // their own.
             // a size above 6 keeps its extra bits' top 6 in the record and the rest in a
-            // continuation right after it (kernels.hpp; the fast path fixes such blocks up
-            // in cont(), from the record's low 6 bits)
+            // continuation right after it (kernels.hpp); the fast path writes every record
+            // with its extra bits' low 6, and cont() rewrites such lanes' records from their
+            // coefficients
             b.bg = __builtin_amdgcn_ballot_w64(cat > kRecXBits);
             uint32_t x = bits & 63u;
             if constexpr (kExact) {
