@@ -107,7 +107,7 @@ __device__ __forceinline__ uint32_t rec_bits(uint32_t w, uint32_t off, const uin
 
 // every workgroup's WgPlace from the records (the placement scan), kK3Threads threads
 __device__ void place_all(const EntropyArgs& a, uint32_t G, uint32_t* wsum, int tid);
-__device__ void write_wg_record(const EntropyArgs& a, uint32_t wg, uint32_t G, const uint8_t* R8, uint32_t Lb,
+__device__ void write_wg_record(const EntropyArgs& a, uint32_t wg, uint32_t G, uint32_t edge, uint32_t Lb,
                                 const uint32_t* cnt8, uint32_t* flag, uint32_t* wsum, int tid);
 
 template <int kN>
@@ -160,6 +160,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
     };
     uint32_t pend = 0;
     bool has_pend = false;
+    uint32_t head = 0;  // (thread 0) the stream's first 8 bits, from its first complete word
     uint64_t tq = JPGE_NOW();
     // Records through a buffer descriptor over this workgroup's tiles: every round
     // issues its next load unconditionally (past the end: an out-of-range offset,
@@ -288,6 +289,7 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
             if (ncw) {
                 const uint32_t w0 = L.stage[0] | L.carry;
                 if (has_pend) count_word(pend, w0);
+                else head = w0 >> 24;
                 pend = ncw == 1 ? w0 : L.stage[ncw - 1];
                 has_pend = true;
             }
@@ -306,9 +308,19 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
         JPGE_ACC(2, tq);
     }
     const uint32_t Lb = wl;  // this workgroup's bits (>= 6: every block codes >= 2 bits, >= 3 blocks)
-    if (tid == 0 && (Lb & 31)) R32[Lb >> 5] = __builtin_bswap32(L.carry);
-    vm_drain();
-    __syncthreads();
+    // (thread 0) the stream's first and last 8 bits for the record, from the last complete
+    // word and the partial one in registers: nothing reads R back, so no wave waits here
+    // for its region stores to complete (the pack kernel reads R after the launch boundary).
+    // A stream shorter than a byte (a 4:4:4 restart interval of one MCU) is only ever
+    // placed byte-aligned: its "last 8 bits" are its bits, right-aligned.
+    uint32_t edge = 0;
+    if (tid == 0) {
+        const uint32_t r = Lb & 31, carry = L.carry;
+        if (r) R32[Lb >> 5] = __builtin_bswap32(carry);
+        if (!has_pend) head = carry >> 24;
+        const uint32_t tail = ((has_pend ? pend << r : 0u) | (r ? carry >> (32 - r) : 0u)) & 0xFFu;
+        edge = head | (tail << 8);
+    }
     JPGE_STAMP(1);
 
     // ---- 0xFF bytes of the stream at each byte alignment b ----
@@ -334,31 +346,20 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
         }
     }
     __syncthreads();
-    write_wg_record(a, wg, G, R8, Lb, L.cnt8, &L.carry, &L.wsum[0][0], tid);
+    write_wg_record(a, wg, G, edge, Lb, L.cnt8, &L.carry, &L.wsum[0][0], tid);
     JPGE_STAMP(2);
 }
 
 // The workgroup's record {bits, edge bits, ff[8]} for the pack kernel, and (a.done)
 // the placement of every workgroup by the last one to finish.  flag: a scratch LDS
 // word; wsum: 16 LDS words, 8-byte aligned (place_all's 64-bit scans).
-__device__ void write_wg_record(const EntropyArgs& a, uint32_t wg, uint32_t G, const uint8_t* R8, uint32_t Lb,
+__device__ void write_wg_record(const EntropyArgs& a, uint32_t wg, uint32_t G, uint32_t edge, uint32_t Lb,
                                 const uint32_t* cnt8, uint32_t* flag, uint32_t* wsum, int tid) {
     if (tid < 3) {
         uint32_t* rec = reinterpret_cast<uint32_t*>(a.rec + (uint64_t)wg * kEntropyRecordBytes);
         uint4 v;
         if (tid == 0) {
-            // first 8 bits; last 8 bits (the 16-bit window holding them is inside R).
-            // A stream shorter than a byte (a 4:4:4 restart interval of one MCU) is
-            // only ever placed byte-aligned: its "last 8 bits" are its bits, right-aligned.
-            const uint32_t head = R8[0];
-            uint32_t tail;
-            if (Lb >= 8) {
-                const uint32_t s0 = Lb - 8, byte = s0 >> 3, sh = s0 & 7;
-                tail = ((((uint32_t)R8[byte] << 8) | R8[byte + 1]) >> (8 - sh)) & 0xFF;
-            } else {
-                tail = (uint32_t)R8[0] >> (8 - Lb);
-            }
-            v = make_uint4(Lb, head | (tail << 8), 0u, 0u);
+            v = make_uint4(Lb, edge, 0u, 0u);  // (thread 0's first 8 bits | last 8 bits << 8)
         } else {
             const int b0 = 4 * (tid - 1);  // ff[0..3], ff[4..7]
             v = make_uint4(cnt8[b0], cnt8[b0 + 1], cnt8[b0 + 2], cnt8[b0 + 3]);
