@@ -298,10 +298,14 @@ __global__ __launch_bounds__(kK3Threads) __attribute__((amdgpu_waves_per_eu(kK3W
             L.carry = v;
         }
         // the stage words used back to zero once everyone has read them (the stage
-        // starts zeroed, so the rounds OR records in without a zeroing barrier)
-        lds_barrier();
-        for (uint32_t w = tid; w <= ncw; w += kK3Threads) L.stage[w] = 0;
-        lds_barrier();
+        // starts zeroed, so the rounds OR records in without a zeroing barrier); after
+        // the last round nothing reuses the stage (thread 0 alone reads its carry)
+        const bool more = r0 + kRound < total;
+        if (more) {
+            lds_barrier();
+            for (uint32_t w = tid; w <= ncw; w += kK3Threads) L.stage[w] = 0;
+            lds_barrier();
+        }
         wl += pos - lead;
         lead = wl & 31;
         pos = lead;
@@ -807,7 +811,7 @@ __global__ __launch_bounds__(kK3Threads) void entropy_pack_kernel(FrameSet<Entro
             }
         }
         d += clen;
-        __syncthreads();  // ob is rewritten by the next round
+        if (c + kChunk < n_own) __syncthreads();  // ob is rewritten by the next round
     }
     if (last && tid == 0) {
         uint64_t len = 0;  // end of the image (EOI written) or of the stripe's bytes
