@@ -144,19 +144,21 @@ def spawn(n: int, argv: list[str]) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    # (children reaped in the order they end, so the rank that failed first names the
+    # status, not a peer that failed because it vanished)
     rc = 0
-    live = list(procs)
+    live = {p.pid: p for p in procs}
     while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                for q in live:  # (our own children, by handle)
-                    q.terminate()
-        time.sleep(0.05)
+        pid, status = os.waitpid(-1, 0)
+        p = live.pop(pid, None)
+        if p is None:
+            continue
+        code = os.waitstatus_to_exitcode(status)
+        p.returncode = code
+        if code != 0 and rc == 0:
+            rc = code if code > 0 else 128 - code
+            for q in live.values():  # (our own children, by handle)
+                q.terminate()
     return rc
 
 
